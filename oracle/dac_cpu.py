@@ -1,0 +1,71 @@
+"""ORACLE — CPU restatement of DACAutoencoder.decode (44.1 kHz DAC decoder). TEST INFRASTRUCTURE ONLY.
+
+Restates, with the same ATen ops, the third-party path the reference calls
+(`zonos/autoencoder.py:25-27` -> transformers `DacModel.decode`):
+
+  from_codes      modeling_dac.py:347-371  (codebook gather -> 1x1 out_proj, summed over 9 codebooks)
+  DacDecoder      modeling_dac.py:407-441  (conv k7 -> 4 x DecoderBlock -> Snake -> conv k7 -> tanh)
+  DacDecoderBlock modeling_dac.py:236-264  (Snake -> ConvTranspose(k=2s, s, p=ceil(s/2)) -> 3 x ResUnit)
+  DacResidualUnit modeling_dac.py:175-209  (Snake -> conv k7 dil d -> Snake -> conv 1x1 -> + skip)
+  Snake1d         modeling_dac.py:86-100   (x + 1/(a+1e-9) * sin(a x)^2)
+
+The CPU reference runs fp32 (autocast is disabled on CPU, autoencoder.py:26), so this is the
+fp32 oracle; the GPU path is compared to it with the tolerance stated in its test.
+Pinned against transformers' own DacModel in tests/golden (make_golden.py, `dac_*` fixtures).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+STRIDES = (8, 8, 4, 2)
+DILATIONS = (1, 3, 9)
+
+
+def snake(x: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    shp = x.shape
+    x = x.reshape(shp[0], shp[1], -1)
+    x = x + (alpha + 1e-9).reciprocal() * torch.sin(alpha * x).pow(2)
+    return x.reshape(shp)
+
+
+class OracleDAC:
+    def __init__(self, weights: dict):
+        self.w = weights
+
+    def from_codes(self, codes: torch.Tensor) -> torch.Tensor:
+        q = 0.0
+        for i in range(codes.shape[1]):
+            p = f"quantizer.quantizers.{i}."
+            lat = F.embedding(codes[:, i, :], self.w[p + "codebook.weight"]).transpose(1, 2)
+            q = q + F.conv1d(lat, self.w[p + "out_proj.weight"], self.w[p + "out_proj.bias"])
+        return q
+
+    def _res_unit(self, x, p, dil):
+        y = F.conv1d(snake(x, self.w[p + "snake1.alpha"]), self.w[p + "conv1.weight"], self.w[p + "conv1.bias"],
+                     dilation=dil, padding=3 * dil)
+        y = F.conv1d(snake(y, self.w[p + "snake2.alpha"]), self.w[p + "conv2.weight"], self.w[p + "conv2.bias"])
+        pad = (x.shape[-1] - y.shape[-1]) // 2
+        if pad > 0:
+            x = x[..., pad:-pad]
+        return x + y
+
+    def decoder(self, z: torch.Tensor) -> torch.Tensor:
+        h = F.conv1d(z, self.w["decoder.conv1.weight"], self.w["decoder.conv1.bias"], padding=3)
+        for j, s in enumerate(STRIDES):
+            p = f"decoder.block.{j}."
+            h = snake(h, self.w[p + "snake1.alpha"])
+            h = F.conv_transpose1d(h, self.w[p + "conv_t1.weight"], self.w[p + "conv_t1.bias"], stride=s,
+                                   padding=math.ceil(s / 2))
+            for u, d in enumerate(DILATIONS):
+                h = self._res_unit(h, p + f"res_unit{u + 1}.", d)
+        h = snake(h, self.w["decoder.snake1.alpha"])
+        h = F.conv1d(h, self.w["decoder.conv2.weight"], self.w["decoder.conv2.bias"], padding=3)
+        return torch.tanh(h)
+
+    @torch.inference_mode()
+    def decode(self, codes: torch.Tensor) -> torch.Tensor:
+        """autoencoder.py:25-27 on CPU: [B, 9, T] int64 -> [B, 1, 512 T] fp32."""
+        return self.decoder(self.from_codes(codes)).squeeze(1).unsqueeze(1).float()

@@ -1,0 +1,81 @@
+"""Pin the CPU oracle against fixtures produced by the reference itself (tests/golden/make_golden.py)."""
+import hashlib
+
+import pytest
+import torch
+
+from oracle import zonos_cpu as oz
+from oracle.dac_cpu import OracleDAC
+from tests.helpers import dac_weights, load_golden, synthetic_weights
+from zonos_vibes_amd.config import ZonosConfig
+
+
+def test_delay_pattern_matches_reference():
+    t, _ = load_golden("delay_pattern")
+    d = oz.apply_delay_pattern(t["codes"], 1025)
+    assert torch.equal(d, t["delayed"])
+    assert torch.equal(oz.revert_delay_pattern(d), t["reverted"])
+
+
+def test_penalty_and_greedy_match_reference():
+    t, _ = load_golden("penalty_greedy")
+    pen = oz.repetition_penalty(t["logits"].clone(), t["generated"], 3.0, 2)
+    assert torch.equal(pen, t["penalized"])
+    g = oz.sample(t["logits"].clone(), temperature=0.0, generated=t["generated"])
+    assert torch.equal(g, t["greedy"])
+
+
+def test_samplers_match_reference_with_its_own_noise():
+    t, meta = load_golden("samplers")
+    for i, ps in enumerate(meta["params"]):
+        out = oz.sample(t["logits"].clone(), generated=t["generated"], noise=t[f"q{i}"], **oz.sample_params(ps))
+        assert torch.equal(out, t[f"out{i}"]), ps
+
+
+def test_rope_table_bits():
+    t, meta = load_golden("rope")
+    fc = oz.rope_table(16384, 128)
+    assert hashlib.sha256(fc.numpy().tobytes()).hexdigest() == meta["sha256"]
+    assert torch.equal(fc[:8], t["rows_0_8"])
+
+
+@pytest.mark.parametrize("case_idx", range(5))
+def test_tiny_trajectories(case_idx):
+    t, meta = load_golden("tiny_trajectories")
+    cfg = ZonosConfig.from_dict(meta["cfg"])
+    case = meta["cases"][case_idx]
+    w = synthetic_weights(cfg, **case["model_kw"])
+    m = oz.OracleZonos(cfg, w)
+    tag = case["tag"]
+    prefix = t.get(tag + "/prefix")
+    torch.set_num_threads(4)
+    torch.manual_seed(case["seed"])
+    out = m.generate(t[tag + "/cond"], prefix, max_new_tokens=case["n"], sampling_params=case["params"])
+    assert torch.equal(out, t[tag + "/codes"]), tag
+
+
+def test_full_width_layer_logits():
+    t, meta = load_golden("full_layer")
+    cfg = ZonosConfig.from_dict(meta["cfg"])
+    m = oz.OracleZonos(cfg, synthetic_weights(cfg, zero_eos=True))
+    torch.set_num_threads(meta["threads"])
+    with torch.inference_mode():
+        cache = m.new_cache(2, 16 + 8 + 9)
+        delayed = oz.apply_delay_pattern(torch.full((1, 9, 8), -1), 1025)
+        pl = m.prefill(t["cond"], delayed[..., :1], cache, 2.0)
+        cache["offset"] += 17
+        cache["lengths"][:] += 17
+        assert torch.equal(pl, t["prefill_logits"])
+        for s in range(3):
+            lg = m.decode_one(t["feed"][s], cache, torch.tensor(2.0))
+            cache["offset"] += 1
+            cache["lengths"][:] += 1
+            assert torch.equal(lg, t["step_logits"][s]), s
+
+
+def test_dac_decode_matches_transformers():
+    t, meta = load_golden("dac_decode")
+    torch.set_num_threads(meta["threads"])
+    wav = OracleDAC(dac_weights()).decode(t["codes"])
+    assert wav.shape == t["wav"].shape
+    torch.testing.assert_close(wav, t["wav"], rtol=0, atol=1e-6)

@@ -1,0 +1,106 @@
+"""Model configuration mirror of the reference's `zonos/config.py`.
+
+Same dataclass names and field meanings as the reference so that a `config.json`
+written for `Zonos.from_local` (reference `zonos/model.py:65-88`) loads unchanged:
+
+* `BackboneConfig`          -> reference `zonos/config.py:28-39`
+* `PrefixConditionerConfig` -> reference `zonos/config.py:42-45`
+* `ZonosConfig.from_dict`   -> reference `zonos/config.py:48-62`
+
+Only the fields the hot path reads are interpreted. The prefix conditioner is out of
+scope; its config is carried through untouched.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, asdict
+from typing import Any
+
+# Token constants of the 44.1 kHz DAC codebooks (reference `zonos/config.py:50-52`).
+N_CODEBOOKS = 9
+CODEBOOK_SIZE = 1024
+EOS_TOKEN = 1024
+MASK_TOKEN = 1025
+EMB_VOCAB = 1026          # nn.Embedding(1026, d)   reference model.py:36
+HEAD_VOCAB = 1025         # nn.Linear(d, 1025)      reference model.py:37
+HEAD_VOCAB_PADDED = 1026  # pad_weight_ adds 1025 % 8 = 1 zero row (utils.py:12-27)
+DAC_HOP = 512
+DAC_SAMPLE_RATE = 44100
+ROPE_TABLE_LEN = 16384    # precompute_freqs_cis(16384, hd)  reference _torch.py:67
+
+
+@dataclass
+class BackboneConfig:
+    d_model: int = 1024
+    d_intermediate: int = 0
+    attn_mlp_d_intermediate: int = 0
+    n_layer: int = 16
+    ssm_cfg: dict = field(default_factory=dict)
+    attn_layer_idx: list = field(default_factory=list)
+    attn_cfg: dict = field(default_factory=dict)
+    rms_norm: bool = False
+    residual_in_fp32: bool = False
+    norm_epsilon: float = 1e-5
+
+    @property
+    def num_heads(self) -> int:
+        return int(self.attn_cfg["num_heads"])
+
+    @property
+    def num_heads_kv(self) -> int:
+        return int(self.attn_cfg["num_heads_kv"])
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.num_heads
+
+
+@dataclass
+class PrefixConditionerConfig:
+    conditioners: list = field(default_factory=list)
+    projection: str = "none"
+
+
+@dataclass
+class ZonosConfig:
+    backbone: BackboneConfig
+    prefix_conditioner: PrefixConditionerConfig
+    eos_token_id: int = EOS_TOKEN
+    masked_token_id: int = MASK_TOKEN
+    pad_vocab_to_multiple_of: int = 8
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "ZonosConfig":
+        d = dict(d)
+        bb = BackboneConfig(**d.pop("backbone"))
+        pc = PrefixConditionerConfig(**d.pop("prefix_conditioner", {"conditioners": [], "projection": "none"}))
+        return cls(bb, pc, **d)
+
+    def to_dict(self) -> dict[str, Any]:
+        return asdict(self)
+
+
+def transformer_config(d_model: int, n_layer: int, num_heads: int, num_heads_kv: int, d_ff: int,
+                       eps: float = 1e-5) -> ZonosConfig:
+    """A transformer-backbone `ZonosConfig` (the `torch` backbone, reference _torch.py:52-80)."""
+    bb = BackboneConfig(
+        d_model=d_model, d_intermediate=0, attn_mlp_d_intermediate=d_ff, n_layer=n_layer, ssm_cfg={},
+        attn_layer_idx=[], attn_cfg={"causal": True, "num_heads": num_heads, "num_heads_kv": num_heads_kv,
+                                     "rotary_emb_dim": d_model // num_heads},
+        rms_norm=False, residual_in_fp32=False, norm_epsilon=eps)
+    return ZonosConfig(bb, PrefixConditionerConfig([], "none"))
+
+
+def zonos_v01_transformer() -> ZonosConfig:
+    """Zonos-v0.1-transformer dims (d=2048, L=26, H=16/4, FFN=8192)."""
+    return transformer_config(2048, 26, 16, 4, 8192)
+
+
+def tiny_transformer(n_layer: int = 2) -> ZonosConfig:
+    """Small config used by the parity fixtures (head_dim stays 128, GQA group 4)."""
+    return transformer_config(512, n_layer, 4, 1, 1024)
+
+
+PRESETS = {
+    "zonos-v0.1-transformer": zonos_v01_transformer,
+    "tiny": tiny_transformer,
+}
