@@ -1,0 +1,233 @@
+"""Headline benchmark: real-time factor of Zonos-v0.1-transformer generate() + DAC decode on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): one utterance per GPU per step —
+batch=1, Lc=160 synthetic prefix-conditioning rows, 861 new frames (10 s of 44.1 kHz audio),
+greedy decode with the reference's default repetition penalty, EOS suppressed (row 1024 of
+heads.0 zeroed) so every step decodes exactly 869 backbone steps, then DAC decode of the 861
+frames. Synthetic hash-PRNG weights at the full 1.6 B-parameter transformer dims.
+A "step" = one full utterance (prefill + 869 decode steps + DAC decode).
+value = total audio seconds over all ranks / max-over-ranks wall time of the K timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from zonos_vibes_amd import _lib  # noqa: E402
+from zonos_vibes_amd import synthetic as syn  # noqa: E402
+from zonos_vibes_amd.config import DAC_HOP, DAC_SAMPLE_RATE, zonos_v01_transformer  # noqa: E402
+
+LC, N_NEW = 160, 861
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+BASELINE_RTF = 2.0     # "~2x" real-time on RTX 4090 (README.md:84)
+
+
+def cond_tensor(seed: int, d: int, dev):
+    import numpy as np
+    a = syn.synthetic_conditioning_np(seed, 2, LC, d)
+    return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
+
+
+def time_dominant_kernel(model, reps: int = 3):
+    """fc1 GEMV (+LN prologue, SwiGLU epilogue) of every layer, timed with HIP events on the engine stream.
+
+    Rotating over all 26 layers' 67 MB weights (1.7 GB) keeps the stream out of the 256 MiB
+    Infinity Cache, so the bytes come from HBM as in the decode step.
+    """
+    e = model.engine
+    items = [item for kind, item in e.plan if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(e.stream):
+        for it in items:
+            e._run_gemv(it)
+        start.record(e.stream)
+        for _ in range(reps):
+            for it in items:
+                e._run_gemv(it)
+        end.record(e.stream)
+    end.synchronize()
+    n = reps * len(items)
+    us = start.elapsed_time(end) * 1000.0 / n
+    bytes_launch = 2 * e.F * e.d * 2 + e.R * e.d * 2 + e.R * e.F * 2 + 2 * e.d * 2
+    return us, bytes_launch
+
+
+def time_decode_step(model, steps: int = 64):
+    e = model.engine
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(e.stream):
+        start.record(e.stream)
+        e.step(steps)
+        end.record(e.stream)
+    end.synchronize()
+    return start.elapsed_time(end) * 1000.0 / steps
+
+
+def step_bytes(model, pos: int) -> int:
+    e = model.engine
+    qkv = (e.H + 2 * e.Hkv) * e.hd
+    w = e.L * 2 * (qkv * e.d + e.d * e.H * e.hd + 2 * e.F * e.d + e.d * e.F) + 9 * 1025 * e.d * 2
+    kv = e.R * e.L * e.Hkv * e.hd * 2 * 2 * (pos + 1)
+    return w + kv
+
+
+def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
+    """The oracle (PyTorch eager CPU, same op order as the reference) on a bounded sample of C2."""
+    from oracle.dac_cpu import OracleDAC
+    from oracle.zonos_cpu import OracleZonos, apply_delay_pattern
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    w = {k: v.cpu() for k, v in dev_weights.items()}
+    m = OracleZonos(cfg, w)
+    cond = cond_tensor(1, cfg.backbone.d_model, "cpu")
+    with torch.inference_mode():
+        cache = m.new_cache(2, LC + N_NEW + 9)
+        delayed = apply_delay_pattern(torch.full((1, 9, N_NEW), -1), 1025)
+        t0 = time.perf_counter()
+        m.prefill(cond, delayed[..., :1], cache, 2.0)
+        t_pre = time.perf_counter() - t0
+        cache["offset"] += LC + 1
+        cache["lengths"][:] += LC + 1
+        n, t0 = 0, time.perf_counter()
+        ids = torch.randint(0, 1024, (1, 9, 1))
+        while n < 8 or (time.perf_counter() - t0 < budget_s * 0.6 and n < 200):
+            m.decode_one(ids, cache, torch.tensor(2.0))
+            cache["offset"] += 1
+            cache["lengths"][:] += 1
+            n += 1
+        t_step = (time.perf_counter() - t0) / n
+        dac = OracleDAC({k: v for k, v in _dac_weights_cpu().items()})
+        nf = 43
+        t0 = time.perf_counter()
+        dac.decode(torch.randint(0, 1024, (1, 9, nf)))
+        t_dac = (time.perf_counter() - t0) / nf
+    total = t_pre + (N_NEW + 8) * t_step + N_NEW * t_dac
+    audio = N_NEW * DAC_HOP / DAC_SAMPLE_RATE
+    return {"value": round(audio / total, 4), "unit": "x realtime (audio s / CPU s), extrapolated",
+            "cores": threads, "kind": "port",
+            "sample": f"C2 prefill (2x{LC + 1} rows) {t_pre:.2f}s + {n} of {N_NEW + 8} decode steps "
+                      f"({t_step * 1e3:.1f} ms/step) + DAC decode of {nf} of {N_NEW} frames "
+                      f"({t_dac * 1e3:.1f} ms/frame), extrapolated to the full utterance"}
+
+
+def _dac_weights_cpu():
+    return dict(syn.iter_torch_cpu(syn.dac_specs(), 0))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--new-tokens", type=int, default=N_NEW)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    n_new = args.new_tokens
+    model = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n_new + 9, max_prefill=LC + 1)
+    cond = cond_tensor(1 + rank, cfg.backbone.d_model, dev)
+    params = dict(temperature=0.0)
+
+    def one_utterance():
+        codes = model.generate(cond, max_new_tokens=n_new, sampling_params=params, progress_bar=False, chunk=128)
+        wav = model.autoencoder.decode(codes)
+        return codes, wav
+
+    for _ in range(args.warmup):
+        codes, wav = one_utterance()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    frames = 0
+    for _ in range(args.steps):
+        codes, wav = one_utterance()
+        frames += codes.shape[-1]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert codes.shape[-1] == n_new and wav.shape[-1] == n_new * DAC_HOP, (codes.shape, wav.shape)
+    if dist:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        fr = torch.tensor([frames], device=dev, dtype=torch.float64)
+        dist.all_reduce(fr)
+        frames = int(fr.item())
+    audio_s = frames * DAC_HOP / DAC_SAMPLE_RATE
+    rtf = audio_s / elapsed
+
+    # kernel-level measurement (outside the timed region)
+    us, bl = time_dominant_kernel(model)
+    step_us = time_decode_step(model)
+    out = None
+    if rank == 0:
+        achieved = bl / (us * 1e-6) / 1e9
+        out = {
+            "metric": "real-time factor (44kHz audio s/compute s) + DAC tokens/s/GPU, Zonos-transformer",
+            "value": round(rtf, 3), "unit": "x realtime (audio s / wall s, all GPUs)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(rtf / BASELINE_RTF, 3),
+            "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"C2: batch=1 per GPU, Lc={LC}, {n_new} frames ({n_new * DAC_HOP / DAC_SAMPLE_RATE:.2f}"
+                                   f" s audio), greedy + rep. penalty, EOS suppressed, + DAC decode",
+                       "global_batch": world, "seq_len": LC + n_new + 9, "parallelism": f"dp{world} (utterance-sharded)",
+                       "decode_steps": n_new + 8},
+            "dac_tokens_per_s_per_gpu": round(frames * 9 / elapsed / world, 1),
+            "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
+            "decode_step_us": round(step_us, 1),
+            "decode_step_hbm_frac": round(step_bytes(model, LC + n_new) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
+            "roofline": {"kernel": "gemv_kernel<MT=1,NF=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": None, "avg_us": round(us, 2),
+                         "bytes_per_launch": bl},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sd = {}
+            for sp in syn.zonos_specs(cfg):
+                t = torch.empty(sp.shape, dtype=torch.bfloat16, device=dev)
+                _lib.check(_lib.lib().zmi_fill_uniform(t.data_ptr(), sp.numel, syn.tensor_key(0, sp.name), sp.scale,
+                                                       sp.offset, 0, torch.cuda.current_stream().cuda_stream))
+                sd[sp.name] = t
+            sd["heads.0.weight"][1024] = 0
+            torch.cuda.synchronize()
+            out["cpu_baseline"] = cpu_baseline(sd, cfg)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * zonos_hip.h — C ABI of libzonos_hip.so, the MI355X (gfx950) hot path of Zonos generate() +
+ * DACAutoencoder.decode().
+ *
+ * The reference (BreakTheBeta/Zonos_Vibes) is pure Python with no FFI; its device work is
+ * ATen ops called from the functions cited below. This ABI is the boundary the Python host
+ * (zonos_vibes_amd/) binds with ctypes to replace them. Conventions:
+ *   - every pointer is a device pointer owned by the caller (allocated by torch), unless noted;
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
+ *   - every function returns 0 on success or a nonzero status; zmi_last_error() explains it;
+ *   - no function allocates or synchronises, so every launcher can be hipGraph-captured.
+ */
+#ifndef ZONOS_HIP_H
+#define ZONOS_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------
+ * Weight-streaming GEMV / skinny GEMM:  out[m, n] = sum_k A[m, k] W[n, k]  (+ fused epilogue)
+ * Replaces nn.Linear in zonos/backbone/_torch.py:114-115 (in_proj/out_proj), :147-152 (fc1/fc2)
+ * and zonos/model.py:100-101 (apply_heads); the LayerNorm prologue replaces nn.LayerNorm at
+ * _torch.py:62,88,90 (norm, norm2, norm_f).
+ * ------------------------------------------------------------------------------------- */
+enum {
+  ZMI_EPI_STORE = 0,    /* out bf16 [M][ldo]                                                   */
+  ZMI_EPI_RESIDUAL = 1, /* out bf16 [M][ldo] += bf16(acc)          (_torch.py:100-101)          */
+  ZMI_EPI_QKV = 2,      /* q -> out, rope(k) / v -> KV cache        (_torch.py:18-49, 117-126)  */
+  ZMI_EPI_SWIGLU = 3,   /* out bf16 [M][F] = y * silu(gate)        (_torch.py:150-152)          */
+  ZMI_EPI_LOGITS = 4,   /* out f32 [M][9][1026] = bf16(acc).float() (model.py:100-101,111)      */
+  ZMI_EPI_F32 = 5       /* out f32 [M][ldo] raw fp32 sums (tests)                              */
+};
+enum { ZMI_PACK_IDENTITY = 0, ZMI_PACK_SWIGLU = 1 };
+
+typedef struct ZmiGemvArgs {
+  const void* W;        /* packed weight (zmi_pack_weight)                                    */
+  const void* X;        /* bf16 [M][ldx] activations                                          */
+  int M, N, K, ldx;     /* N = packed (padded) columns, multiple of 16; K multiple of 128       */
+  int ksplit;           /* <= 0: library plan (depends on N, K only)                           */
+  int nchunk;           /* filled by the library                                               */
+  const void* ln_w;     /* bf16 [K] LayerNorm weight, or NULL for a plain GEMV                */
+  const void* ln_b;     /* bf16 [K] LayerNorm bias                                             */
+  float eps;
+  void* out;
+  int ldo;
+  int n_valid;          /* real (unpadded) columns                                             */
+  const int* row_kv;    /* QKV: [M] KV-cache row of each activation row                        */
+  const int* row_pos;   /* QKV: [M] position (<0: inactive row, nothing written)               */
+  void* k_cache;        /* QKV: bf16 [rows][hkv][smax][hd] for this layer                      */
+  void* v_cache;
+  int smax, hq, hkv, hd;
+  const float* rope;    /* [16384][hd/2][2] (cos, sin) fp32 (_torch.py:9-15)                  */
+  float* slab;          /* split-K workspace, zmi_gemv_slab_floats() floats                    */
+  unsigned* counters;   /* split-K arrival tickets, zero-initialised, re-armed by the kernel   */
+} ZmiGemvArgs;
+
+int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
+int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
+int64_t zmi_gemv_slab_floats(int M, int N, int K);
+
+/* ---------------------------------------------------------------------------------------
+ * Attention: GQA scaled-dot-product attention over the KV cache, one query position per
+ * (query row). Replaces F.scaled_dot_product_attention(q, k, v, is_causal, enable_gqa)
+ * at zonos/backbone/_torch.py:136 for decode (1 query) and prefill (causal = position bound).
+ * ------------------------------------------------------------------------------------- */
+int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
+                  const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
+                  int ldo, float* partials, unsigned* counters, void* stream);
+int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
+
+/* ---------------------------------------------------------------------------------------
+ * Sampler + EOS state machine + delay-pattern frame write, per utterance slot.
+ * Replaces model.py:112-115 (CFG), :266-267/280 (EOS logit bias), sampling.py:99-182
+ * (repetition penalty, greedy / softmax / unified / top-p / top-k / min-p / exponential race)
+ * and model.py:283-299 (EOS diagonal, masked_scatter_ frame compaction, counters).
+ * ------------------------------------------------------------------------------------- */
+typedef struct ZmiSampling {
+  float temperature, top_p, min_p, linear, conf, quad, rep_penalty, cfg_scale;
+  int top_k, rep_window;
+  uint64_t seed;
+} ZmiSampling;
+
+typedef struct ZmiSlots {
+  int* active;      /* [S] 1 while generating                                              */
+  int* pos;         /* [S] tokens in the KV cache (= next position)                         */
+  int* offset;      /* [S] last written delayed-frame index (reference `offset`)            */
+  int* remaining;   /* [S] reference `remaining_steps`                                      */
+  int* stopping;    /* [S] reference `stopping`                                             */
+  int* step;        /* [S] decode steps done                                                */
+  int* delayed;     /* [S][9][tcap] delayed codes (int32; -1 unknown, 1024 EOS, 1025 mask)   */
+  const ZmiSampling* params; /* [S]                                                           */
+  const int* total_len; /* [S] delayed length P + N + 9 (frames at or past it are not written) */
+  int tcap;
+  int n_slots;
+} ZmiSlots;
+
+/* mode 0 = decode step (bias + penalty + FSM), 1 = prefill (no bias, no penalty, no FSM) */
+int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
+                    unsigned* counters, int mode, int slot_begin, int slot_count, void* stream);
+/* x[2s], x[2s+1] = sum_k emb_k[delayed[s][k][offset[s]]]  (model.py:97-98,142) and the
+ * per-row (kv row, position) tables of the step (-1 position for inactive slots). */
+int zmi_embed_step(const ZmiSlots* slots, const void* emb, int d, void* x, int* row_kv, int* row_pos,
+                   void* stream);
+/* prefill embedding rows: x[s] = sum_k emb_k[codes[k][s]] for s < n (model.py:195) */
+int zmi_embed_codes(const int* codes, int ld_codes, int n, const void* emb, int d, void* x, int ldx, void* stream);
+/* delayed[slot] = apply_delay_pattern(prefix codes | -1)    (codebook_pattern.py:5-7)      */
+int zmi_delay_init(const ZmiSlots* slots, int slot, const int* prefix, int prefix_len, int total_len, void* stream);
+/* out[9][T] int64 = revert_delay_pattern(delayed[slot]) with >=1024 -> 0 (model.py:309-311) */
+int zmi_delay_revert(const ZmiSlots* slots, int slot, int64_t* out, int t_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * DAC 44.1 kHz decoder (DACAutoencoder.decode, autoencoder.py:25-27 -> transformers DacModel).
+ * Activations are fp16, channels-last [T][C]; weights fp16 packed per tap [tap][Co][Ci].
+ * ------------------------------------------------------------------------------------- */
+/* z[t][c] = sum_i (out_proj_i(codebook_i[codes[i][t]]))   (modeling_dac.py:347-371)          */
+int zmi_dac_from_codes(const int64_t* codes, int T, const float* codebooks, const float* proj_w,
+                       const float* proj_b, void* z, void* stream);
+/* out[t_out][co] = epi( bias + sum_tap sum_ci W[tap][co][ci] * x[t_in][ci] ) with
+ *   t_in = q + in_off + tap * tap_step, t_out = q * out_stride + out_phase, q in [0, n_out)
+ * epilogue: + skip (fp16, optional), store raw (optional) and/or snake(alpha) (optional). */
+int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* bias, int c_out, int taps,
+                 int tap_step, int in_off, int n_out, int out_stride, int out_phase, int t_out, const void* skip,
+                 void* out_raw, void* out_snake, const float* alpha, void* stream);
+/* final Snake'd [T][96] -> conv k7 (96->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441)    */
+int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Synthetic weights: fill with the counter-based uniform stream of zonos_vibes_amd/synthetic.py
+ * dtype 0 = bf16, 1 = f32.
+ * ------------------------------------------------------------------------------------- */
+int zmi_fill_uniform(void* dst, int64_t n, uint64_t key, float scale, float offset, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * hipGraph helpers: capture whatever the caller enqueues on `stream` between begin/end and
+ * replay it. The decode step (~130 launches) is captured once per batch geometry.
+ * ------------------------------------------------------------------------------------- */
+int zmi_graph_begin(void* stream);
+int zmi_graph_end(void* stream, void** graph_exec);
+int zmi_graph_launch(void* graph_exec, int times, void* stream);
+int zmi_graph_destroy(void* graph_exec);
+
+const char* zmi_last_error(void);
+int zmi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZONOS_HIP_H */

@@ -1,0 +1,111 @@
+"""ctypes binding of libzonos_hip.so (the C ABI declared in include/zonos_hip.h).
+
+The library is built in-tree (zonos_vibes_amd/build.py). There is no fallback: if the
+shared object is missing or a call fails, a RuntimeError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzonos_hip.so")
+
+c_int, c_int64, c_float, c_void_p, c_uint64 = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, \
+    ctypes.c_uint64
+c_int_p = ctypes.POINTER(ctypes.c_int)
+
+EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
+PACK_IDENTITY, PACK_SWIGLU = 0, 1
+
+
+class GemvArgs(ctypes.Structure):
+    _fields_ = [
+        ("W", c_void_p), ("X", c_void_p),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("ldx", c_int),
+        ("ksplit", c_int), ("nchunk", c_int),
+        ("ln_w", c_void_p), ("ln_b", c_void_p), ("eps", c_float),
+        ("out", c_void_p), ("ldo", c_int), ("n_valid", c_int),
+        ("row_kv", c_void_p), ("row_pos", c_void_p),
+        ("k_cache", c_void_p), ("v_cache", c_void_p),
+        ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
+        ("rope", c_void_p), ("slab", c_void_p), ("counters", c_void_p),
+    ]
+
+
+class Sampling(ctypes.Structure):
+    _fields_ = [
+        ("temperature", c_float), ("top_p", c_float), ("min_p", c_float), ("linear", c_float),
+        ("conf", c_float), ("quad", c_float), ("rep_penalty", c_float), ("cfg_scale", c_float),
+        ("top_k", c_int), ("rep_window", c_int), ("seed", c_uint64),
+    ]
+
+
+class Slots(ctypes.Structure):
+    _fields_ = [
+        ("active", c_void_p), ("pos", c_void_p), ("offset", c_void_p), ("remaining", c_void_p),
+        ("stopping", c_void_p), ("step", c_void_p), ("delayed", c_void_p), ("params", c_void_p),
+        ("total_len", c_void_p), ("tcap", c_int), ("n_slots", c_int),
+    ]
+
+
+_SIGS = {
+    "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
+    "zmi_gemv_slab_floats": (c_int64, [c_int, c_int, c_int]),
+    "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                c_void_p]),
+    "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_embed_codes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "zmi_delay_init": (c_int, [ctypes.POINTER(Slots), c_int, c_void_p, c_int, c_int, c_void_p]),
+    "zmi_delay_revert": (c_int, [ctypes.POINTER(Slots), c_int, c_void_p, c_int, c_void_p]),
+    "zmi_dac_from_codes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_dac_conv": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
+    "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),
+    "zmi_graph_begin": (c_int, [c_void_p]),
+    "zmi_graph_end": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "zmi_graph_launch": (c_int, [c_void_p, c_int, c_void_p]),
+    "zmi_graph_destroy": (c_int, [c_void_p]),
+    "zmi_last_error": (ctypes.c_char_p, []),
+    "zmi_version": (c_int, []),
+}
+
+EXPORTED = sorted(_SIGS)
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the library (torch is imported first so its HIP runtime is the one in use)."""
+    import torch  # noqa: F401  -- libamdhip64.so.7 from torch must be resident before the dlopen
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -m zonos_vibes_amd.build` "
+                           "(the HIP path has no CPU fallback)")
+    lib_ = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib_, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib_
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = load()
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().zmi_last_error().decode(errors="replace")
+        raise RuntimeError(f"libzonos_hip {what} failed (status {rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    return None if t is None else t.data_ptr()

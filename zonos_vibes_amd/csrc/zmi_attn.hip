@@ -1,0 +1,213 @@
+// GQA attention over the KV cache for decode (one query per row) and prefill (causal),
+// gfx950. Replaces F.scaled_dot_product_attention(..., enable_gqa=True) at
+// reference zonos/backbone/_torch.py:136 (scale 1/sqrt(hd); causal for the prefill).
+//
+// One workgroup = (query, kv head, chunk of CH=64 key positions). The G = Hq/Hkv query heads
+// of the group share every K/V row the block reads (K/V bytes are read once per group):
+//   scores : 4 lanes per key row, each 64 contiguous bytes of K (16 B/lane loads), G dots,
+//            2-step lane reduction;
+//   softmax: one wave per head, lane = key position (wave-reduced max / sum);
+//   P.V    : lane pair-of-dims over a V row (one 256 B row per wave instruction).
+// Chunk partials (m, l, o[hd]) are merged by the last-arriving chunk in chunk order, so the
+// result depends only on the position, never on batch size or scheduling (batch-invariant).
+// KV layout: [row][kv head][position][hd] bf16, contiguous per (row, head) stream.
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+
+namespace {
+
+constexpr int CH = 64;
+constexpr int HD = 128;
+
+struct AttnArgs {
+  const bf16_t* q;
+  int ldq;
+  const bf16_t* k;
+  const bf16_t* v;
+  const int* kv_row;
+  const int* pos;
+  int hkv, smax, maxch;
+  float scale;
+  bf16_t* out;
+  int ldo;
+  float* part;
+  unsigned* counters;
+};
+
+template <int G>
+__global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
+  __shared__ float qs[G][HD];
+  __shared__ float sc[G][CH];
+  __shared__ float opart[4][G][HD];
+  __shared__ float mlv[G][2];
+  __shared__ unsigned last_flag;
+
+  const int qi = blockIdx.x / a.hkv, kh = blockIdx.x - qi * a.hkv, c = blockIdx.y;
+  const int pos = a.pos[qi];
+  if (pos < 0) return;
+  const int nch = pos / CH + 1;
+  if (c >= nch) return;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const size_t kvbase = ((size_t)a.kv_row[qi] * a.hkv + kh) * a.smax * HD;
+
+  for (int e = t; e < G * HD / 2; e += 256) {
+    const int g = e / (HD / 2), d = (e % (HD / 2)) * 2;
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(a.q + (size_t)qi * a.ldq + (kh * G + g) * HD + d);
+    qs[g][d] = bf2f(v);
+    qs[g][d + 1] = bf2f(v >> 16);
+  }
+  __syncthreads();
+
+  // ---- scores: thread -> (key row p, quarter of the head dim) ----
+  {
+    const int pl = t >> 2, qq = t & 3;
+    const int p = c * CH + pl;
+    float dot[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) dot[g] = 0.f;
+    if (p <= pos) {
+      const uint4* kr = reinterpret_cast<const uint4*>(a.k + kvbase + (size_t)p * HD + qq * 32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 kv = kr[i];
+        const uint32_t u[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float k0 = bf2f(u[j]), k1 = bf2f(u[j] >> 16);
+          const int d = qq * 32 + i * 8 + j * 2;
+#pragma unroll
+          for (int g = 0; g < G; ++g) dot[g] += qs[g][d] * k0 + qs[g][d + 1] * k1;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      dot[g] += __shfl_xor(dot[g], 1, 64);
+      dot[g] += __shfl_xor(dot[g], 2, 64);
+    }
+    if (qq == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) sc[g][pl] = (p <= pos) ? dot[g] * a.scale : -INFINITY;
+    }
+  }
+  __syncthreads();
+
+  // ---- chunk softmax: one wave per head ----
+  for (int g = wave; g < G; g += 4) {
+    const float s = sc[g][lane];
+    const float m = wave_max(s);
+    const float e = (s == -INFINITY) ? 0.f : expf(s - m);
+    const float l = wave_sum(e);
+    sc[g][lane] = e;
+    if (lane == 0) {
+      mlv[g][0] = m;
+      mlv[g][1] = l;
+    }
+  }
+  __syncthreads();
+
+  // ---- P.V: thread -> (dim pair, position phase) ----
+  {
+    const int dp = lane * 2, ph = wave;
+    float o0[G], o1[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) o0[g] = o1[g] = 0.f;
+    const int plim = min(CH, pos - c * CH + 1);
+    for (int pl = ph; pl < plim; pl += 4) {
+      const uint32_t vv = *reinterpret_cast<const uint32_t*>(a.v + kvbase + (size_t)(c * CH + pl) * HD + dp);
+      const float v0 = bf2f(vv), v1 = bf2f(vv >> 16);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        o0[g] += sc[g][pl] * v0;
+        o1[g] += sc[g][pl] * v1;
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      opart[ph][g][dp] = o0[g];
+      opart[ph][g][dp + 1] = o1[g];
+    }
+  }
+  __syncthreads();
+
+  const int g_t = t / (256 / G);             // finalising thread -> (head, dims)
+  const int nd = HD / (256 / G);              // dims per thread
+  const int d_t = (t % (256 / G)) * nd;
+  if (nch == 1) {
+    const float inv_l = 1.0f / mlv[g_t][1];
+    for (int i = 0; i < nd; ++i) {
+      const int d = d_t + i;
+      const float o = ((opart[0][g_t][d] + opart[1][g_t][d]) + opart[2][g_t][d]) + opart[3][g_t][d];
+      a.out[(size_t)qi * a.ldo + (kh * G + g_t) * HD + d] = (bf16_t)f2bf(o * inv_l);
+    }
+    return;
+  }
+
+  // ---- publish chunk partial; last chunk merges in chunk order ----
+  const size_t pstride = (size_t)G * (HD + 2);
+  float* base = a.part + (size_t)blockIdx.x * a.maxch * pstride;
+  for (int e = t; e < G * HD; e += 256) {
+    const int g = e / HD, d = e % HD;
+    base[c * pstride + g * (HD + 2) + 2 + d] =
+        ((opart[0][g][d] + opart[1][g][d]) + opart[2][g][d]) + opart[3][g][d];
+  }
+  if (t < G) {
+    base[c * pstride + t * (HD + 2)] = mlv[t][0];
+    base[c * pstride + t * (HD + 2) + 1] = mlv[t][1];
+  }
+  if (!zmi_last_arriver(a.counters + blockIdx.x, (unsigned)nch, &last_flag)) return;
+
+  float mmax = -INFINITY;
+  for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, base[cc * pstride + g_t * (HD + 2)]);
+  float L = 0.f;
+  float o[HD / (256 / G) > 0 ? HD / (256 / G) : 1];
+  for (int i = 0; i < nd; ++i) o[i] = 0.f;
+  for (int cc = 0; cc < nch; ++cc) {
+    const float* pc = base + cc * pstride + g_t * (HD + 2);
+    const float w = expf(pc[0] - mmax);
+    L += w * pc[1];
+    for (int i = 0; i < nd; ++i) o[i] += w * pc[2 + d_t + i];
+  }
+  const float inv_l = 1.0f / L;
+  for (int i = 0; i < nd; ++i)
+    a.out[(size_t)qi * a.ldo + (kh * G + g_t) * HD + d_t + i] = (bf16_t)f2bf(o[i] * inv_l);
+}
+
+}  // namespace
+
+extern "C" int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos) {
+  const int maxch = max_pos / CH + 1;
+  return (int64_t)n_query * hkv * maxch * (hq / hkv) * (hd + 2);
+}
+
+extern "C" int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
+                             const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
+                             int ldo, float* partials, unsigned* counters, void* stream) {
+  if (hd != HD) return zmi_fail_msg("attention: head_dim must be 128");
+  if (max_pos >= smax) return zmi_fail_msg("attention: max_pos must be < smax");
+  AttnArgs a;
+  a.q = (const bf16_t*)q;
+  a.ldq = ldq;
+  a.k = (const bf16_t*)k_cache;
+  a.v = (const bf16_t*)v_cache;
+  a.kv_row = q_kv_row;
+  a.pos = q_pos;
+  a.hkv = hkv;
+  a.smax = smax;
+  a.maxch = max_pos / CH + 1;
+  a.scale = 1.0f / sqrtf((float)hd);
+  a.out = (bf16_t*)out;
+  a.ldo = ldo;
+  a.part = partials;
+  a.counters = counters;
+  dim3 grid(n_query * hkv, a.maxch);
+  hipStream_t s = (hipStream_t)stream;
+  switch (hq / hkv) {
+    case 1: hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(attn_kernel<2>, grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(attn_kernel<4>, grid, dim3(256), 0, s, a); break;
+    default: return zmi_fail_msg("attention: unsupported GQA group (1, 2, 4)");
+  }
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

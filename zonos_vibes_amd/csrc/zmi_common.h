@@ -1,0 +1,90 @@
+// Common device helpers for the Zonos MI355X (gfx950 / CDNA4) hot path.
+//
+// Numerics conventions (mirroring the reference's bf16 rounding points):
+//   * every GEMM output is rounded to bf16 before any consumer sees it (nn.Linear in bf16),
+//   * elementwise fp32 math is written without fused multiply-adds where the reference
+//     evaluates separate tensor ops (the library is compiled with -ffp-contract=off),
+//   * bf16 rounding is round-to-nearest-even.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef uint16_t f16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+#define ZMI_WAVE 64
+
+__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float((h & 0xffffu) << 16); }
+
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return ((u >> 16) | 0x40u) & 0xffffu;  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+// round-trip through bf16
+__device__ __forceinline__ float bfround(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ float h2f(uint32_t h) {
+  _Float16 v = __builtin_bit_cast(_Float16, (uint16_t)(h & 0xffffu));
+  return (float)v;
+}
+__device__ __forceinline__ uint32_t f2h(float f) {
+  _Float16 v = (_Float16)f;
+  return (uint32_t)__builtin_bit_cast(uint16_t, v);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// splitmix64 finaliser (shared with zonos_vibes_amd/synthetic.py)
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// ---- inter-workgroup hand-off (cdna_hip_programming.md §6 Guideline 16 recipe) ----------
+// Producer: all waves drained, barrier, one lane releases (agent) and bumps the ticket.
+// Returns true in every thread of the block that drew the last ticket; that block then
+// acquires (agent) before plain-loading the other blocks' slabs.
+__device__ __forceinline__ bool zmi_last_arriver(unsigned* counter, unsigned total, unsigned* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned last = (t == total - 1) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for next launch
+    }
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+#define ZMI_CHECK(expr)                                                     \
+  do {                                                                      \
+    hipError_t _e = (expr);                                                 \
+    if (_e != hipSuccess) return zmi_fail(_e, #expr, __FILE__, __LINE__);   \
+  } while (0)
+
+int zmi_fail(hipError_t e, const char* what, const char* file, int line);
+int zmi_fail_msg(const char* msg);

@@ -1,0 +1,205 @@
+// DAC 44.1 kHz decoder conv stack on MFMA, gfx950 (DACAutoencoder.decode, reference
+// zonos/autoencoder.py:25-27 -> transformers DacModel.decode, modeling_dac.py:610-640).
+//
+// Every convolution of the decoder (k7 dilated convs, 1x1 convs, the k=2s transposed convs
+// in polyphase form) is one implicit GEMM:
+//     out[t_out][co] = epi( bias[co] + sum_tap sum_ci W[tap][co][ci] * x[t_in][ci] )
+//     t_in = q + in_off + tap * tap_step,  t_out = q * out_stride + out_phase
+// Activations are channels-last fp16 so both MFMA operands are 16 B contiguous per lane:
+//   A (weights) lane l: co = l&15, ci = 8*(l>>4)..+7      B (activations) lane l: t = l&15, same ci
+// fp32 accumulation (v_mfma_f32_16x16x32_f16), fp16 storage as the reference's GPU autocast.
+// Snake (x + sin^2(a x)/(a + 1e-9), modeling_dac.py:86-100) is evaluated ONCE per element in
+// the producing epilogue, which stores the raw tensor (for the residual skip) and/or its
+// Snake'd copy (the next conv's input); the residual add of DacResidualUnit
+// (modeling_dac.py:189-209) is fused in the 1x1 conv's epilogue.
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+
+namespace {
+
+struct ConvArgs {
+  const f16_t* x;
+  int t_in, c_in;
+  const f16_t* w;
+  const float* bias;
+  int c_out, taps, tap_step, in_off, n_out, out_stride, out_phase, t_out;
+  const f16_t* skip;
+  f16_t* out_raw;
+  f16_t* out_snake;
+  const float* alpha;
+};
+
+__device__ __forceinline__ float snake(float y, float a) {
+  const float s = sinf(a * y);
+  return y + (1.0f / (a + 1e-9f)) * (s * s);
+}
+
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int co0 = blockIdx.y * (32 * WM) + wm * (16 * WM);
+  const int q0 = blockIdx.x * (32 * WN) + wn * (16 * WN);
+  const int kq = (lane >> 4) * 8, lr = lane & 15;
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int tap = 0; tap < a.taps; ++tap) {
+    int tin[WN];
+    bool ok[WN];
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int q = q0 + j * 16 + lr;
+      tin[j] = q + a.in_off + tap * a.tap_step;
+      ok[j] = q < a.n_out && tin[j] >= 0 && tin[j] < a.t_in;
+    }
+    const f16_t* wt = a.w + ((size_t)tap * a.c_out + co0 + lr) * a.c_in + kq;
+    for (int ci = 0; ci < a.c_in; ci += 32) {
+      uint4 af[WM], bfr[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const uint4*>(wt + (size_t)i * 16 * a.c_in + ci);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        bfr[j] = ok[j] ? *reinterpret_cast<const uint4*>(a.x + (size_t)tin[j] * a.c_in + ci + kq)
+                       : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, af[i]),
+                                                             __builtin_bit_cast(f16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: lane holds 4 consecutive output channels of one time step
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int q = q0 + j * 16 + lr;
+    if (q >= a.n_out) continue;
+    const size_t to = (size_t)q * a.out_stride + a.out_phase;
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const int co = co0 + i * 16 + kq / 2;  // (lane>>4)*4
+      float y[4];
+      uint2 sk = {0u, 0u};
+      if (a.skip) sk = *reinterpret_cast<const uint2*>(a.skip + to * a.c_out + co);
+      const uint32_t su[2] = {sk.x, sk.y};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        y[r] = acc[i][j][r] + a.bias[co + r];
+        if (a.skip) y[r] = y[r] + h2f(su[r >> 1] >> ((r & 1) * 16));
+      }
+      if (a.out_raw) {
+        uint2 o;
+        o.x = f2h(y[0]) | (f2h(y[1]) << 16);
+        o.y = f2h(y[2]) | (f2h(y[3]) << 16);
+        *reinterpret_cast<uint2*>(a.out_raw + to * a.c_out + co) = o;
+      }
+      if (a.out_snake) {
+        float z[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = snake(y[r], a.alpha[co + r]);
+        uint2 o;
+        o.x = f2h(z[0]) | (f2h(z[1]) << 16);
+        o.y = f2h(z[2]) | (f2h(z[3]) << 16);
+        *reinterpret_cast<uint2*>(a.out_snake + to * a.c_out + co) = o;
+      }
+    }
+  }
+}
+
+// quantizer.from_codes (modeling_dac.py:347-371): 9 x [codebook gather (8-d) -> 1x1 conv to 1024 + bias], summed
+__global__ __launch_bounds__(256) void from_codes_kernel(const int64_t* codes, int T, const float* cbooks,
+                                                          const float* pw, const float* pb, f16_t* z) {
+  const int t = blockIdx.x;
+  __shared__ float lat[ZMI_NCB][8];
+  if (threadIdx.x < ZMI_NCB * 8) {
+    const int i = threadIdx.x >> 3, j = threadIdx.x & 7;
+    int64_t tok = codes[(size_t)i * T + t];
+    tok = tok < 0 ? 0 : (tok > 1023 ? 1023 : tok);
+    lat[i][j] = cbooks[((size_t)i * 1024 + tok) * 8 + j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 1024; c += 256) {
+    float acc = 0.f;
+    for (int i = 0; i < ZMI_NCB; ++i) {
+      float s = 0.f;
+      const float* wr = pw + ((size_t)i * 1024 + c) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += wr[j] * lat[i][j];
+      acc = acc + (s + pb[i * 1024 + c]);
+    }
+    z[(size_t)t * 1024 + c] = (f16_t)f2h(acc);
+  }
+}
+
+// decoder.conv2 (96 -> 1, k7, pad 3) + tanh (modeling_dac.py:438-441); input already Snake'd
+__global__ __launch_bounds__(256) void conv_out_kernel(const f16_t* x, int T, int c_in, const float* w, float bias,
+                                                        float* out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  float acc = 0.f;
+  for (int k = 0; k < 7; ++k) {
+    const int ti = t + k - 3;
+    if (ti < 0 || ti >= T) continue;
+    const f16_t* xr = x + (size_t)ti * c_in;
+    for (int c = 0; c < c_in; c += 8) {
+      const uint4 v = *reinterpret_cast<const uint4*>(xr + c);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc += w[(c + 2 * j) * 7 + k] * h2f(u[j]);
+        acc += w[(c + 2 * j + 1) * 7 + k] * h2f(u[j] >> 16);
+      }
+    }
+  }
+  out[t] = tanhf(acc + bias);
+}
+
+}  // namespace
+
+extern "C" int zmi_dac_from_codes(const int64_t* codes, int T, const float* codebooks, const float* proj_w,
+                                  const float* proj_b, void* z, void* stream) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(from_codes_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, codes, T, codebooks, proj_w,
+                     proj_b, (f16_t*)z);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* bias, int c_out, int taps,
+                            int tap_step, int in_off, int n_out, int out_stride, int out_phase, int t_out,
+                            const void* skip, void* out_raw, void* out_snake, const float* alpha, void* stream) {
+  if (c_in % 32) return zmi_fail_msg("dac_conv: c_in % 32");
+  if (n_out <= 0) return 0;
+  if ((size_t)(n_out - 1) * out_stride + out_phase >= (size_t)t_out) return zmi_fail_msg("dac_conv: output bounds");
+  ConvArgs a{(const f16_t*)x, t_in, c_in, (const f16_t*)w, bias, c_out, taps, tap_step, in_off, n_out,
+             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha};
+  hipStream_t s = (hipStream_t)stream;
+  if (c_out % 128 == 0) {
+    dim3 grid((n_out + 127) / 128, c_out / 128);
+    hipLaunchKernelGGL((conv_kernel<4, 4>), grid, dim3(256), 0, s, a);
+  } else if (c_out % 96 == 0) {
+    dim3 grid((n_out + 127) / 128, c_out / 96);
+    hipLaunchKernelGGL((conv_kernel<3, 4>), grid, dim3(256), 0, s, a);
+  } else if (c_out % 32 == 0) {
+    dim3 grid((n_out + 127) / 128, c_out / 32);
+    hipLaunchKernelGGL((conv_kernel<1, 4>), grid, dim3(256), 0, s, a);
+  } else {
+    return zmi_fail_msg("dac_conv: c_out must be a multiple of 32");
+  }
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream) {
+  if (c_in % 8) return zmi_fail_msg("dac_conv_out: c_in % 8");
+  hipLaunchKernelGGL(conv_out_kernel, dim3((t + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const f16_t*)x, t,
+                     c_in, w, bias, out);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,441 @@
+// Per-step token selection and frame bookkeeping for every active utterance slot, gfx950.
+//
+// One workgroup per (codebook, slot) computes, over the 1026-entry vocabulary:
+//   CFG            u + (c - u) * cfg, column 1025 = -inf          reference model.py:112-115
+//   EOS bias       -inf on EOS for codebooks 1..8 (decode only)    model.py:266-267,280
+//   rep. penalty   3^count over the last `window` delayed tokens   sampling.py:99-114,164-165
+//   greedy         argmax, first index on ties                      sampling.py:180
+//   stochastic     softmax(l/T) -> [unified] -> [top-p] -> [top-k] -> [min-p] -> argmax(p/q),
+//                  q ~ Exp(1) from a counter-based hash (or a caller noise buffer)  sampling.py:4-96,167-178
+// The last of the 9 codebook workgroups of a slot (in-launch ticket) then runs the EOS state
+// machine and the delay-pattern frame write with the reference's masked_scatter_ compaction
+// (model.py:283-299): the k-th still-unknown (-1) slot of the frame gets the k-th token.
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+
+namespace {
+
+constexpr int NV = ZMI_VOCAB;   // 1026
+constexpr int PER = 5;          // ceil(1026 / 256)
+constexpr int SORTN = 2048;
+
+struct SampleArgs {
+  ZmiSlots sl;
+  const float* logits;
+  const float* noise;
+  int* next;
+  unsigned* counters;
+  int mode;
+  int slot_begin;
+};
+
+__device__ float block_reduce_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+__device__ float block_reduce_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+// argmax with first-index tie break
+__device__ int block_argmax(float v, int idx, float* redv, int* redi) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    redv[w] = v;
+    redi[w] = idx;
+  }
+  __syncthreads();
+  float bv = redv[0];
+  int bi = redi[0];
+  for (int i = 1; i < 4; ++i)
+    if (redv[i] > bv || (redv[i] == bv && redi[i] < bi)) {
+      bv = redv[i];
+      bi = redi[i];
+    }
+  return bi;
+}
+
+__device__ void bitonic_desc(uint64_t* keys) {
+  for (int k = 2; k <= SORTN; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < SORTN; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = keys[i], y = keys[ixj];
+          const bool first_desc = (i & k) == 0;
+          if (first_desc ? (x < y) : (x > y)) {
+            keys[i] = y;
+            keys[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// Sort probs descending (ties: lower index first) into keys; returns nothing.
+__device__ void sort_probs(const float* probs, uint64_t* keys) {
+  for (int i = threadIdx.x; i < SORTN; i += 256) {
+    const float p = i < NV ? probs[i] : 0.f;
+    keys[i] = ((uint64_t)__float_as_uint(p) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+  }
+  __syncthreads();
+  bitonic_desc(keys);
+}
+
+__device__ __forceinline__ float key_prob(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+__device__ __forceinline__ int key_index(uint64_t k) { return (int)(0xFFFFFFFFu - (uint32_t)k); }
+
+__device__ void renormalize(float* probs, float* red) {
+  float s = 0.f;
+  for (int v = threadIdx.x; v < NV; v += 256) s += probs[v];
+  s = block_reduce_sum(s, red);
+  __syncthreads();
+  for (int v = threadIdx.x; v < NV; v += 256) probs[v] = probs[v] / s;
+  __syncthreads();
+}
+
+__device__ void softmax_inplace(float* x, float* red) {
+  float m = -INFINITY;
+  for (int v = threadIdx.x; v < NV; v += 256) m = fmaxf(m, x[v]);
+  m = block_reduce_max(m, red);
+  float s = 0.f;
+  for (int v = threadIdx.x; v < NV; v += 256) {
+    const float e = expf(x[v] - m);
+    x[v] = e;
+    s += e;
+  }
+  s = block_reduce_sum(s, red);
+  __syncthreads();
+  for (int v = threadIdx.x; v < NV; v += 256) x[v] = x[v] / s;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
+  __shared__ float probs[NV + 2];
+  __shared__ uint64_t keys[SORTN];
+  __shared__ double dscan[256];
+  __shared__ float red[4];
+  __shared__ float redv[4];
+  __shared__ int redi[4];
+  __shared__ unsigned last_flag;
+
+  const int cb = blockIdx.x, s = a.slot_begin + blockIdx.y, t = threadIdx.x;
+  if (!a.sl.active[s]) return;
+  const ZmiSampling P = a.sl.params[s];
+  const int lrow = 2 * blockIdx.y;
+  const float* lc = a.logits + ((size_t)lrow * ZMI_NCB + cb) * NV;
+  const float* lu = a.logits + ((size_t)(lrow + 1) * ZMI_NCB + cb) * NV;
+  const bool decode = a.mode == 0;
+  const int* dl = a.sl.delayed + ((size_t)s * ZMI_NCB + cb) * a.sl.tcap;
+  const int o = a.sl.offset[s] + 1;  // frame written this step
+
+  // ---- CFG, padding, EOS bias, repetition penalty ----
+  int win_lo = 0, win_hi = 0;
+  if (decode && P.rep_penalty != 1.0f) {
+    win_hi = o;
+    win_lo = max(0, o - P.rep_window);
+  }
+  for (int i = 0; i < PER; ++i) {
+    const int v = t + i * 256;
+    if (v >= NV) break;
+    const float c = lc[v], u = lu[v];
+    float l = u + (c - u) * P.cfg_scale;
+    if (v >= 1025) l = -INFINITY;
+    if (decode) l = l + ((cb >= 1 && v == ZMI_EOS) ? -INFINITY : 0.0f);
+    if (win_hi > win_lo) {
+      float f = 1.0f;
+      for (int j = win_lo; j < win_hi; ++j)
+        if (min(dl[j], NV - 1) == v) f = f * P.rep_penalty;
+      l = (l <= 0.f) ? l * f : l / f;
+    }
+    probs[v] = l;
+  }
+  __syncthreads();
+
+  int tok;
+  if (P.temperature <= 0.f) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = t; v < NV; v += 256)
+      if (probs[v] > bv || bi == 0x7fffffff) {
+        bv = probs[v];
+        bi = v;
+      }
+    tok = block_argmax(bv, bi, redv, redi);
+  } else {
+    for (int v = t; v < NV; v += 256) probs[v] = probs[v] / P.temperature;
+    __syncthreads();
+    softmax_inplace(probs, red);
+    if (P.linear > 0.f) {  // unified sampler (sampling.py:29-43)
+      float ent = 0.f;
+      for (int v = t; v < NV; v += 256) {
+        const float lp = logf(fmaxf(probs[v], 1e-20f));
+        ent += probs[v] * lp;
+      }
+      ent = -block_reduce_sum(ent, red);
+      __syncthreads();
+      for (int v = t; v < NV; v += 256) {
+        const float lp = logf(fmaxf(probs[v], 1e-20f));
+        probs[v] = lp * (P.linear + ent * P.conf) - (lp * lp) * P.quad;
+      }
+      __syncthreads();
+      softmax_inplace(probs, red);
+    }
+    if (P.top_p > 0.f) {  // sampling.py:64-79: keep sorted i unless cumsum_i - p_i > top_p
+      sort_probs(probs, keys);
+      double run = 0.0;
+      double loc[SORTN / 256];
+      for (int j = 0; j < SORTN / 256; ++j) {
+        run += (double)key_prob(keys[t * (SORTN / 256) + j]);
+        loc[j] = run;
+      }
+      dscan[t] = run;
+      __syncthreads();
+      if (t == 0) {  // exclusive scan of the 256 thread totals, in order
+        double acc = 0.0;
+        for (int i = 0; i < 256; ++i) {
+          const double x = dscan[i];
+          dscan[i] = acc;
+          acc += x;
+        }
+      }
+      __syncthreads();
+      for (int j = 0; j < SORTN / 256; ++j) {
+        const int i = t * (SORTN / 256) + j;
+        if (i >= NV) break;
+        const uint64_t k = keys[i];
+        const float p = key_prob(k);
+        const float csum = (float)(dscan[t] + loc[j]);
+        if (csum - p > P.top_p) probs[key_index(k)] = 0.f;
+      }
+      __syncthreads();
+      renormalize(probs, red);
+    }
+    if (P.top_k > 0) {  // sampling.py:45-61
+      sort_probs(probs, keys);
+      const int kk = min(P.top_k, NV);
+      const float pivot = key_prob(keys[kk - 1]);
+      for (int v = t; v < NV; v += 256)
+        if (probs[v] < pivot) probs[v] = 0.f;
+      __syncthreads();
+      renormalize(probs, red);
+    }
+    if (P.min_p > 0.f) {  // sampling.py:82-96
+      float m = 0.f;
+      for (int v = t; v < NV; v += 256) m = fmaxf(m, probs[v]);
+      m = block_reduce_max(m, red);
+      const float thr = P.min_p * m;
+      __syncthreads();
+      for (int v = t; v < NV; v += 256)
+        if (probs[v] < thr) probs[v] = 0.f;
+      __syncthreads();
+      renormalize(probs, red);
+    }
+    // exponential race: argmax(p / q), q ~ Exp(1)  (sampling.py:19-21)
+    const uint64_t ctr_base = ((uint64_t)(decode ? a.sl.step[s] + 1 : 0) * ZMI_NCB + cb) * NV;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = t; v < NV; v += 256) {
+      float q;
+      if (a.noise) {
+        q = a.noise[((size_t)blockIdx.y * ZMI_NCB + cb) * NV + v];
+      } else {
+        const uint64_t z = mix64(P.seed + 0x9E3779B97F4A7C15ull * (ctr_base + v + 1));
+        const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        q = -logf(u);
+      }
+      const float r = probs[v] / q;
+      if (r > bv || bi == 0x7fffffff) {
+        bv = r;
+        bi = v;
+      }
+    }
+    tok = block_argmax(bv, bi, redv, redi);
+  }
+
+  if (t == 0) a.next[(size_t)s * ZMI_NCB + cb] = tok;
+  if (!zmi_last_arriver(a.counters + s, ZMI_NCB, &last_flag)) return;
+
+  // ---- EOS state machine + frame compaction write (one thread per slot) ----
+  if (t != 0) return;
+  int nt[ZMI_NCB];
+  for (int k = 0; k < ZMI_NCB; ++k) nt[k] = a.next[(size_t)s * ZMI_NCB + k];
+  int rem = a.sl.remaining[s];
+  int stop = a.sl.stopping[s];
+  if (decode) {
+    if (nt[0] == ZMI_EOS) {
+      rem = min(rem, 9);
+      stop = 1;
+    }
+    if (stop) {
+      const int idx = min(9 - rem, 8);
+      for (int k = 0; k < idx; ++k) nt[k] = ZMI_MASK;
+      nt[idx] = ZMI_EOS;
+    }
+  }
+  if (o < a.sl.total_len[s]) {
+    int kk = 0;
+    for (int k = 0; k < ZMI_NCB; ++k) {
+      int* cell = a.sl.delayed + ((size_t)s * ZMI_NCB + k) * a.sl.tcap + o;
+      if (*cell == -1) *cell = nt[kk++];
+    }
+  }
+  a.sl.offset[s] = o;
+  if (decode) {
+    a.sl.pos[s] += 1;
+    rem -= 1;
+    a.sl.remaining[s] = rem;
+    a.sl.stopping[s] = stop;
+    a.sl.step[s] += 1;
+    if (rem <= 0) a.sl.active[s] = 0;
+  }
+}
+
+// ---- embeddings (model.py:97-98): sum over codebooks 0..8, bf16 rounding after each add ----
+__device__ __forceinline__ void embed_row(const int* toks, const bf16_t* emb, int d, bf16_t* out0, bf16_t* out1) {
+  for (int c = threadIdx.x * 8; c < d; c += 256 * 8) {
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < ZMI_NCB; ++k) {
+      const uint4 e = *reinterpret_cast<const uint4*>(emb + ((size_t)k * ZMI_VOCAB + toks[k]) * d + c);
+      const uint32_t u[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float lo = bf2f(u[j]), hi = bf2f(u[j] >> 16);
+        if (k == 0) {
+          acc[2 * j] = lo;
+          acc[2 * j + 1] = hi;
+        } else {
+          acc[2 * j] = bfround(acc[2 * j] + lo);
+          acc[2 * j + 1] = bfround(acc[2 * j + 1] + hi);
+        }
+      }
+    }
+    uint4 r;
+    r.x = f2bf(acc[0]) | (f2bf(acc[1]) << 16);
+    r.y = f2bf(acc[2]) | (f2bf(acc[3]) << 16);
+    r.z = f2bf(acc[4]) | (f2bf(acc[5]) << 16);
+    r.w = f2bf(acc[6]) | (f2bf(acc[7]) << 16);
+    *reinterpret_cast<uint4*>(out0 + c) = r;
+    if (out1) *reinterpret_cast<uint4*>(out1 + c) = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_step_kernel(const ZmiSlots sl, const bf16_t* emb, int d, bf16_t* x,
+                                                          int* row_kv, int* row_pos) {
+  const int s = blockIdx.x;
+  const int act = sl.active[s];
+  if (threadIdx.x < 2) {
+    row_kv[2 * s + threadIdx.x] = 2 * s + threadIdx.x;
+    row_pos[2 * s + threadIdx.x] = act ? sl.pos[s] : -1;
+  }
+  if (!act) return;
+  int toks[ZMI_NCB];
+  const int off = sl.offset[s];
+  for (int k = 0; k < ZMI_NCB; ++k) {
+    int tk = sl.delayed[((size_t)s * ZMI_NCB + k) * sl.tcap + off];
+    toks[k] = tk < 0 ? 0 : (tk > ZMI_MASK ? ZMI_MASK : tk);
+  }
+  embed_row(toks, emb, d, x + (size_t)(2 * s) * d, x + (size_t)(2 * s + 1) * d);
+}
+
+__global__ __launch_bounds__(256) void embed_codes_kernel(const int* codes, int ld, const bf16_t* emb, int d,
+                                                           bf16_t* x, int ldx) {
+  const int r = blockIdx.x;
+  int toks[ZMI_NCB];
+  for (int k = 0; k < ZMI_NCB; ++k) {
+    int tk = codes[(size_t)k * ld + r];
+    toks[k] = tk < 0 ? 0 : (tk > ZMI_MASK ? ZMI_MASK : tk);
+  }
+  embed_row(toks, emb, d, x + (size_t)r * ldx, nullptr);
+}
+
+// ---- delay pattern (codebook_pattern.py:5-12) ----
+__global__ void delay_init_kernel(const ZmiSlots sl, int slot, const int* prefix, int plen, int total) {
+  const int t = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+  if (t >= sl.tcap) return;
+  const int n_audio = total - ZMI_NCB;  // P + N
+  int v = ZMI_MASK;
+  const int src = t - k - 1;
+  if (t < total && src >= 0 && src < n_audio) v = src < plen ? prefix[(size_t)k * plen + src] : -1;
+  sl.delayed[((size_t)slot * ZMI_NCB + k) * sl.tcap + t] = v;
+}
+
+__global__ void delay_revert_kernel(const ZmiSlots sl, int slot, int64_t* out, int t_out) {
+  const int t = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+  if (t >= t_out) return;
+  const int v = sl.delayed[((size_t)slot * ZMI_NCB + k) * sl.tcap + t + k + 1];
+  out[(size_t)k * t_out + t] = v >= 1024 ? 0 : v;
+}
+
+}  // namespace
+
+extern "C" int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
+                               unsigned* counters, int mode, int slot_begin, int slot_count, void* stream) {
+  if (slot_begin < 0 || slot_begin + slot_count > slots->n_slots) return zmi_fail_msg("sample: slot range");
+  SampleArgs a;
+  a.sl = *slots;
+  a.logits = logits_rows;
+  a.noise = noise;
+  a.next = next_tokens;
+  a.counters = counters;
+  a.mode = mode;
+  a.slot_begin = slot_begin;
+  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, slot_count), dim3(256), 0, (hipStream_t)stream, a);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_embed_step(const ZmiSlots* slots, const void* emb, int d, void* x, int* row_kv, int* row_pos,
+                              void* stream) {
+  if (d % 8) return zmi_fail_msg("embed: d % 8");
+  hipLaunchKernelGGL(embed_step_kernel, dim3(slots->n_slots), dim3(256), 0, (hipStream_t)stream, *slots,
+                     (const bf16_t*)emb, d, (bf16_t*)x, row_kv, row_pos);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_embed_codes(const int* codes, int ld_codes, int n, const void* emb, int d, void* x, int ldx,
+                               void* stream) {
+  if (d % 8 || n <= 0) return zmi_fail_msg("embed_codes: bad shape");
+  hipLaunchKernelGGL(embed_codes_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, codes, ld_codes,
+                     (const bf16_t*)emb, d, (bf16_t*)x, ldx);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_delay_init(const ZmiSlots* slots, int slot, const int* prefix, int prefix_len, int total_len,
+                              void* stream) {
+  if (total_len > slots->tcap || slot < 0 || slot >= slots->n_slots) return zmi_fail_msg("delay_init: bounds");
+  hipLaunchKernelGGL(delay_init_kernel, dim3((slots->tcap + 255) / 256, ZMI_NCB), dim3(256), 0,
+                     (hipStream_t)stream, *slots, slot, prefix, prefix_len, total_len);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_delay_revert(const ZmiSlots* slots, int slot, int64_t* out, int t_out, void* stream) {
+  if (t_out <= 0) return 0;
+  if (t_out + ZMI_NCB > slots->tcap) return zmi_fail_msg("delay_revert: bounds");
+  hipLaunchKernelGGL(delay_revert_kernel, dim3((t_out + 255) / 256, ZMI_NCB), dim3(256), 0, (hipStream_t)stream,
+                     *slots, slot, out, t_out);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,368 @@
+"""HipEngine: device state + launch plan of the Zonos transformer hot path on one MI355X.
+
+Host-side orchestration in Python (PyTorch-ROCm is used only for device memory and the
+stream); every device op goes through the C ABI of libzonos_hip.so. The decode step
+(~5 launches per layer + embed + heads + sampler) is enqueued once under hipGraph capture
+and replayed per step; all per-step state (positions, offsets, EOS state machine) lives on
+the device, so a step needs no host synchronisation (reference zonos/model.py:276-307 syncs
+the host several times per step).
+
+Batch layout: utterance slot s owns activation / KV rows 2s (conditional) and 2s+1
+(unconditional), i.e. the reference's `hidden_states.repeat(2, 1, 1)` CFG pair
+(model.py:142) interleaved per slot. Each slot runs the reference's batch_size=1 semantics.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from . import synthetic as syn
+from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN, ZonosConfig
+
+HEADS_N = N_CODEBOOKS * 1026            # 9 heads x (1025 + 1 pad row), model.py:37 + utils.py:12-27
+HEADS_N_PAD = (HEADS_N + 15) // 16 * 16
+GEMV_COUNTERS = 1 << 16
+
+
+def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
+    """(cos, sin) table in fp32 computed exactly as precompute_freqs_cis (_torch.py:9-15)."""
+    inv = 1.0 / (10000.0 ** (torch.arange(0, hd, 2)[: hd // 2].float() / hd))
+    ang = torch.outer(torch.arange(n, device=inv.device), inv)
+    cis = torch.polar(torch.ones_like(ang), ang)
+    return torch.stack([cis.real, cis.imag], dim=-1).contiguous()
+
+
+@dataclass
+class SamplingParams:
+    """Reference `sample_from_logits` keywords (sampling.py:117-129) + CFG scale + seed."""
+    temperature: float = 1.0
+    top_p: float = 0.0
+    top_k: int = 0
+    min_p: float = 0.0
+    linear: float = 0.0
+    conf: float = 0.0
+    quad: float = 0.0
+    repetition_penalty: float = 3.0
+    repetition_penalty_window: int = 2
+    cfg_scale: float = 2.0
+    seed: int = 0
+
+    @classmethod
+    def from_dict(cls, d: dict, cfg_scale: float, seed: int) -> "SamplingParams":
+        known = {"temperature", "top_p", "top_k", "min_p", "linear", "conf", "quad", "repetition_penalty",
+                 "repetition_penalty_window"}
+        bad = set(d) - known
+        if bad:
+            raise TypeError(f"sample_from_logits() got unexpected keyword argument(s) {sorted(bad)}")
+        return cls(**d, cfg_scale=float(cfg_scale), seed=int(seed))
+
+    def to_c(self) -> _lib.Sampling:
+        return _lib.Sampling(self.temperature, self.top_p, self.min_p, self.linear, self.conf, self.quad,
+                             self.repetition_penalty, self.cfg_scale, int(self.top_k),
+                             int(self.repetition_penalty_window), self.seed & ((1 << 64) - 1))
+
+
+def _round8(n: int) -> int:
+    return n if n % 8 == 0 else n + 8 - n % 8
+
+
+class HipEngine:
+    def __init__(self, cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
+                 max_prefill: int = 512):
+        bb = cfg.backbone
+        if bb.ssm_cfg:
+            raise NotImplementedError("hybrid (mamba-ssm) backbone is not built (SURVEY.md §8f next #1)")
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.d, self.L, self.H, self.Hkv = bb.d_model, bb.n_layer, bb.num_heads, bb.num_heads_kv
+        self.hd = self.d // self.H
+        self.F = bb.attn_mlp_d_intermediate
+        self.eps = float(bb.norm_epsilon)
+        if self.hd != 128:
+            raise ValueError("the HIP attention kernels are built for head_dim 128")
+        self.S = int(max_slots)
+        self.R = 2 * self.S
+        self.smax = min(_round8(int(max_seqlen)), ROPE_TABLE_LEN)
+        self.tcap = self.smax  # delayed frames per slot never exceed KV positions
+        self.max_prefill = int(max_prefill)
+        self.lib = _lib.lib()
+        self.stream = torch.cuda.Stream(self.dev)
+        self.sptr = self.stream.cuda_stream
+        self.w = None
+        self._graph = None
+        self._alloc()
+
+    # ------------------------------------------------------------------ allocation
+    def _alloc(self):
+        d, R, S, dev = self.d, self.R, self.S, self.dev
+        qd = self.H * self.hd
+        z = lambda *shape, dt=torch.bfloat16: torch.zeros(*shape, dtype=dt, device=dev)  # noqa: E731
+        with torch.cuda.stream(self.stream):
+            self.x, self.q, self.attn = z(R, d), z(R, qd), z(R, qd)
+            self.h = z(R, self.F)
+            self.logits = z(R, N_CODEBOOKS, 1026, dt=torch.float32)
+            self.row_kv = z(R, dt=torch.int32)
+            self.row_pos = z(R, dt=torch.int32)
+            self.kc = z(self.L, R, self.Hkv, self.smax, self.hd)
+            self.vc = z(self.L, R, self.Hkv, self.smax, self.hd)
+            slab = 0
+            for n, k in self._gemv_shapes():
+                slab = max(slab, self.lib.zmi_gemv_slab_floats(R, n, k))
+            self.slab = z(max(slab, 1), dt=torch.float32)
+            self.gemv_cnt = z(GEMV_COUNTERS, dt=torch.int32)
+            nq = max(R, 2 * self.max_prefill)
+            self.attn_part = z(self.lib.zmi_attention_partial_floats(nq, self.H, self.Hkv, self.hd, self.smax - 1),
+                               dt=torch.float32)
+            self.attn_cnt = z(nq * self.Hkv, dt=torch.int32)
+            self.samp_cnt = z(S, dt=torch.int32)
+            self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
+            self.st = {k: z(S, dt=torch.int32) for k in
+                       ("active", "pos", "offset", "remaining", "stopping", "step", "total_len")}
+            self.delayed = torch.full((S, N_CODEBOOKS, self.tcap), 1025, dtype=torch.int32, device=dev)
+            self.params = z(S * ctypes.sizeof(_lib.Sampling), dt=torch.uint8)
+            P = self.max_prefill
+            self.x_pre, self.q_pre, self.attn_pre = z(2 * P, d), z(2 * P, qd), z(2 * P, qd)
+            self.h_pre = z(2 * P, self.F)
+            self.row_kv_pre = z(2 * P, dt=torch.int32)
+            self.row_pos_pre = z(2 * P, dt=torch.int32)
+            self.x_last = z(2, d)
+            self.logits_pre = z(2, N_CODEBOOKS, 1026, dt=torch.float32)
+            self.rope = rope_table(self.hd).to(dev)
+        self.slots = _lib.Slots(*(self.st[k].data_ptr() for k in ("active", "pos", "offset", "remaining",
+                                                                      "stopping", "step")),
+                                self.delayed.data_ptr(), self.params.data_ptr(), self.st["total_len"].data_ptr(),
+                                self.tcap, S)
+        self.stream.synchronize()
+
+    def _gemv_shapes(self):
+        qkv = (self.H + 2 * self.Hkv) * self.hd
+        return [(qkv, self.d), (self.d, self.H * self.hd), (2 * self.F, self.d), (self.d, self.F),
+                (HEADS_N_PAD, self.d)]
+
+    # ------------------------------------------------------------------ weights
+    def _pack(self, w: torch.Tensor, n_pad: int, mode: int = _lib.PACK_IDENTITY) -> torch.Tensor:
+        w = w.to(self.dev, torch.bfloat16).contiguous()
+        n_src, k = w.shape
+        out = torch.empty(n_pad * k, dtype=torch.bfloat16, device=self.dev)
+        _lib.check(self.lib.zmi_pack_weight(w.data_ptr(), out.data_ptr(), n_src, k, n_pad, mode, self.sptr), "pack")
+        return out
+
+    def load_state_dict(self, sd: dict):
+        """Reference state_dict names (model.py:22-51, _torch.py:52-152); heads [1025, d] or [1026, d]."""
+        bf = lambda t: t.to(self.dev, torch.bfloat16).contiguous()  # noqa: E731
+        with torch.cuda.stream(self.stream):
+            w = {"emb": torch.stack([bf(sd[f"embeddings.{k}.weight"])[:EMB_VOCAB] for k in range(N_CODEBOOKS)])}
+            qkv_n = (self.H + 2 * self.Hkv) * self.hd
+            layers = []
+            for i in range(self.L):
+                p = f"backbone.layers.{i}."
+                layers.append(dict(
+                    ln1_w=bf(sd[p + "norm.weight"]), ln1_b=bf(sd[p + "norm.bias"]),
+                    qkv=self._pack(sd[p + "mixer.in_proj.weight"], qkv_n),
+                    out=self._pack(sd[p + "mixer.out_proj.weight"], self.d),
+                    ln2_w=bf(sd[p + "norm2.weight"]), ln2_b=bf(sd[p + "norm2.bias"]),
+                    fc1=self._pack(sd[p + "mlp.fc1.weight"], 2 * self.F, _lib.PACK_SWIGLU),
+                    fc2=self._pack(sd[p + "mlp.fc2.weight"], self.d)))
+            w["layers"] = layers
+            w["nf_w"], w["nf_b"] = bf(sd["backbone.norm_f.weight"]), bf(sd["backbone.norm_f.bias"])
+            heads = torch.zeros(HEADS_N, self.d, dtype=torch.bfloat16, device=self.dev)
+            for k in range(N_CODEBOOKS):
+                hw = bf(sd[f"heads.{k}.weight"])[:HEAD_VOCAB]
+                heads[k * 1026: k * 1026 + HEAD_VOCAB] = hw
+            w["heads"] = self._pack(heads, HEADS_N_PAD)
+            del heads
+        self.stream.synchronize()
+        self.w = w
+        self._build_plan()
+
+    def init_synthetic(self, seed: int = 0, zero_eos: bool = False, eos_row_scale: float | None = None):
+        """Materialise the synthetic weights of synthetic.zonos_specs on the GPU (bit-identical to numpy)."""
+        sd = {}
+        with torch.cuda.stream(self.stream):
+            for sp in syn.zonos_specs(self.cfg):
+                t = torch.empty(sp.shape, dtype=torch.bfloat16, device=self.dev)
+                _lib.check(self.lib.zmi_fill_uniform(t.data_ptr(), sp.numel, syn.tensor_key(seed, sp.name),
+                                                     sp.scale, sp.offset, 0, self.sptr), "fill")
+                sd[sp.name] = t
+            h0 = sd["heads.0.weight"]
+            if zero_eos:
+                h0[1024] = 0
+            if eos_row_scale is not None:
+                h0[1024] = (h0[1024].float() * eos_row_scale).to(torch.bfloat16)
+        self.load_state_dict(sd)
+
+    # ------------------------------------------------------------------ launch plan
+    def _gemv(self, W, X, M, N, K, epi, out, ldo, n_valid=None, ln=None, kv=None, ksplit=0, row_kv=None,
+              row_pos=None):
+        a = _lib.GemvArgs()
+        a.W, a.X, a.M, a.N, a.K, a.ldx = W.data_ptr(), X.data_ptr(), M, N, K, K
+        a.ksplit = ksplit
+        if ln is not None:
+            a.ln_w, a.ln_b = ln[0].data_ptr(), ln[1].data_ptr()
+        a.eps = self.eps
+        a.out, a.ldo = out.data_ptr(), ldo
+        a.n_valid = N if n_valid is None else n_valid
+        if kv is not None:
+            a.row_kv, a.row_pos = row_kv.data_ptr(), row_pos.data_ptr()
+            a.k_cache, a.v_cache = kv[0].data_ptr(), kv[1].data_ptr()
+            a.smax, a.hq, a.hkv, a.hd = self.smax, self.H, self.Hkv, self.hd
+            a.rope = self.rope.data_ptr()
+        a.slab, a.counters = self.slab.data_ptr(), self.gemv_cnt.data_ptr()
+        return (a, epi)
+
+    def _run_gemv(self, item):
+        a, epi = item
+        _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
+
+    def _build_plan(self):
+        """Pre-build the decode-step argument blocks (M = all 2*S rows)."""
+        w, R, d, qd = self.w, self.R, self.d, self.H * self.hd
+        qkv_n = (self.H + 2 * self.Hkv) * self.hd
+        plan = []
+        for i, lw in enumerate(w["layers"]):
+            kv = (self.kc[i], self.vc[i])
+            plan.append(("gemv", self._gemv(lw["qkv"], self.x, R, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                            ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv,
+                                            row_pos=self.row_pos)))
+            plan.append(("attn", i))
+            plan.append(("gemv", self._gemv(lw["out"], self.attn, R, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
+            plan.append(("gemv", self._gemv(lw["fc1"], self.x, R, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
+                                            ln=(lw["ln2_w"], lw["ln2_b"]))))
+            plan.append(("gemv", self._gemv(lw["fc2"], self.h, R, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
+        self._heads = self._gemv(w["heads"], self.x, R, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
+                                 n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))
+        self.plan = plan
+        if self._graph is not None:
+            _lib.check(self.lib.zmi_graph_destroy(self._graph))
+            self._graph = None
+
+    def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
+        _lib.check(self.lib.zmi_attention(q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(),
+                                          row_kv.data_ptr(), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
+                                          self.smax, max_pos, out.data_ptr(), self.H * self.hd,
+                                          self.attn_part.data_ptr(), self.attn_cnt.data_ptr(), self.sptr), "attention")
+
+    def enqueue_step(self, noise: torch.Tensor | None = None):
+        """One decode step for every slot (reference model.py:276-307), enqueued on self.stream."""
+        L = self.lib
+        _lib.check(L.zmi_embed_step(ctypes.byref(self.slots), self.w["emb"].data_ptr(), self.d, self.x.data_ptr(),
+                                    self.row_kv.data_ptr(), self.row_pos.data_ptr(), self.sptr), "embed")
+        for kind, item in self.plan:
+            if kind == "gemv":
+                self._run_gemv(item)
+            else:
+                self._attention(item, self.q, self.R, self.row_kv, self.row_pos, self.smax - 1, self.attn)
+        self._run_gemv(self._heads)
+        _lib.check(L.zmi_sample_step(ctypes.byref(self.slots), self.logits.data_ptr(),
+                                     None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
+                                     self.samp_cnt.data_ptr(), 0, 0, self.S, self.sptr), "sample")
+
+    def capture(self):
+        if self._graph is None:
+            _lib.check(self.lib.zmi_graph_begin(self.sptr), "graph_begin")
+            try:
+                self.enqueue_step()
+            finally:
+                g = ctypes.c_void_p()
+                _lib.check(self.lib.zmi_graph_end(self.sptr, ctypes.byref(g)), "graph_end")
+            self._graph = g.value
+        return self._graph
+
+    def step(self, n: int = 1, use_graph: bool = True):
+        if n <= 0:
+            return
+        if use_graph:
+            _lib.check(self.lib.zmi_graph_launch(self.capture(), n, self.sptr), "graph_launch")
+        else:
+            for _ in range(n):
+                self.enqueue_step()
+
+    # ------------------------------------------------------------------ prefill
+    def prefill(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
+                params: SamplingParams, noise: torch.Tensor | None = None):
+        """_prefill + first sample + frame write (reference model.py:240-264) for one slot."""
+        assert 0 <= slot < self.S
+        lc = cond.shape[1]
+        p = 0 if prefix is None else int(prefix.shape[-1])
+        s_len = lc + p + 1
+        total = p + max_new_tokens + 9
+        if s_len > self.max_prefill:
+            raise ValueError(f"prefill length {s_len} > engine max_prefill {self.max_prefill}")
+        if s_len + max_new_tokens + 8 > self.smax or total > self.tcap:
+            raise ValueError("utterance longer than the engine's KV capacity")
+        if cond.shape[0] != 2 or cond.shape[2] != self.d:
+            raise ValueError("prefix_conditioning must be [2 (cond, uncond), Lc, d_model]")
+        L, d, st = self.lib, self.d, self.st
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.stream):
+            cond = cond.to(self.dev, torch.bfloat16)
+            pr = torch.zeros(N_CODEBOOKS, max(p, 1), dtype=torch.int32, device=self.dev)
+            if p:
+                pr[:, :p] = prefix.reshape(N_CODEBOOKS, p).to(self.dev, torch.int32)
+            cp = torch.tensor(bytearray(params.to_c()), dtype=torch.uint8)
+            sz = ctypes.sizeof(_lib.Sampling)
+            self.params[slot * sz:(slot + 1) * sz].copy_(cp)
+            _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
+            xp = self.x_pre[: 2 * s_len]
+            xp[:lc] = cond[0]
+            xp[s_len: s_len + lc] = cond[1]
+            codes = self.delayed[slot]
+            for half in range(2):
+                _lib.check(L.zmi_embed_codes(codes.data_ptr(), self.tcap, p + 1, self.w["emb"].data_ptr(), d,
+                                             xp[half * s_len + lc].data_ptr(), d, self.sptr), "embed_codes")
+            ar = torch.arange(s_len, dtype=torch.int32, device=self.dev)
+            self.row_pos_pre[: 2 * s_len] = torch.cat([ar, ar])
+            self.row_kv_pre[:s_len] = 2 * slot
+            self.row_kv_pre[s_len: 2 * s_len] = 2 * slot + 1
+            self._prefill_layers(2 * s_len, s_len - 1)
+            self.x_last[0] = xp[s_len - 1]
+            self.x_last[1] = xp[2 * s_len - 1]
+            self._run_gemv(self._gemv(self.w["heads"], self.x_last, 2, HEADS_N_PAD, d, _lib.EPI_LOGITS,
+                                      self.logits_pre, 0, n_valid=HEADS_N, ln=(self.w["nf_w"], self.w["nf_b"])))
+            vals = {"active": 1, "pos": s_len, "offset": p, "remaining": max_new_tokens + 8, "stopping": 0,
+                    "step": 0, "total_len": total}
+            for k, v in vals.items():
+                st[k][slot] = v
+            _lib.check(L.zmi_sample_step(ctypes.byref(self.slots), self.logits_pre.data_ptr(),
+                                         None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
+                                         self.samp_cnt.data_ptr(), 1, slot, 1, self.sptr), "sample_prefill")
+        return s_len
+
+    def _prefill_layers(self, m: int, max_pos: int):
+        d, qd = self.d, self.H * self.hd
+        qkv_n = (self.H + 2 * self.Hkv) * self.hd
+        for i, lw in enumerate(self.w["layers"]):
+            self._run_gemv(self._gemv(lw["qkv"], self.x_pre, m, qkv_n, d, _lib.EPI_QKV, self.q_pre, qd,
+                                      ln=(lw["ln1_w"], lw["ln1_b"]), kv=(self.kc[i], self.vc[i]),
+                                      row_kv=self.row_kv_pre, row_pos=self.row_pos_pre, ksplit=1))
+            self._attention(i, self.q_pre, m, self.row_kv_pre, self.row_pos_pre, max_pos, self.attn_pre)
+            self._run_gemv(self._gemv(lw["out"], self.attn_pre, m, d, qd, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
+            self._run_gemv(self._gemv(lw["fc1"], self.x_pre, m, 2 * self.F, d, _lib.EPI_SWIGLU, self.h_pre, self.F,
+                                      ln=(lw["ln2_w"], lw["ln2_b"]), ksplit=1))
+            self._run_gemv(self._gemv(lw["fc2"], self.h_pre, m, d, self.F, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
+
+    # ------------------------------------------------------------------ readback
+    def slot_state(self, slot: int) -> dict:
+        self.stream.synchronize()
+        return {k: int(v[slot].item()) for k, v in self.st.items()}
+
+    def read_codes(self, slot: int) -> torch.Tensor:
+        """revert_delay_pattern, >=1024 -> 0, truncate to offset-9 (model.py:309-311) -> [1, 9, T] int64."""
+        stt = self.slot_state(slot)
+        n_audio = stt["total_len"] - 9
+        k = stt["offset"] - 9  # python slice end `[..., :offset - 9]`, negative when stopped early by a callback
+        t = min(k, n_audio) if k >= 0 else max(n_audio + k, 0)
+        with torch.cuda.stream(self.stream):
+            out = torch.zeros(N_CODEBOOKS, t, dtype=torch.int64, device=self.dev)
+            if t:
+                _lib.check(self.lib.zmi_delay_revert(ctypes.byref(self.slots), slot, out.data_ptr(), t, self.sptr),
+                           "revert")
+        self.stream.synchronize()
+        return out.unsqueeze(0)
+
+    def release(self, slot: int):
+        with torch.cuda.stream(self.stream):
+            self.st["active"][slot] = 0
