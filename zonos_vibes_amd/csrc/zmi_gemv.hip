@@ -106,14 +106,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
         if (r < rows) {
           xv = *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + k0);
           if (PRO == PRO_LN) {
-            const float mean = ln_mean[r], rstd = ln_rstd[r];
+            // torch CPU LayerNorm form: (x * rstd + (-mean * rstd)) * gamma + beta, separate ops
+            const float rstd = ln_rstd[r], nb = -ln_mean[r] * rstd;
             uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
             const uint32_t uw[4] = {lw.x, lw.y, lw.z, lw.w};
             const uint32_t ub[4] = {lb.x, lb.y, lb.z, lb.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float y0 = ((bf2f(u[j]) - mean) * rstd) * bf2f(uw[j]) + bf2f(ub[j]);
-              float y1 = ((bf2f(u[j] >> 16) - mean) * rstd) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
+              float y0 = (bf2f(u[j]) * rstd + nb) * bf2f(uw[j]) + bf2f(ub[j]);
+              float y1 = (bf2f(u[j] >> 16) * rstd + nb) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
               u[j] = f2bf(y0) | (f2bf(y1) << 16);
             }
             xv = uint4{u[0], u[1], u[2], u[3]};
