@@ -26,7 +26,7 @@ def bf16_ulp(x: float) -> float:
 
 
 def greedy_divergence(gpu_delayed: torch.Tensor, oracle: OracleZonos, cond, prefix, n: int,
-                      floor_ulps: float = 2.0):
+                      floor_ulps: float = 8.0):
     """Returns None if the delayed-code arrays are identical, else a dict describing the first
     divergence; raises AssertionError if that divergence happens at a determined decision."""
     trace: list = []

@@ -49,7 +49,23 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   if (c >= nch) return;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const size_t kvbase = ((size_t)a.kv_row[qi] * a.hkv + kh) * a.smax * HD;
+  const int plim = min(CH, pos - c * CH + 1);   // valid keys in this chunk
 
+  // ---- issue every load of the block up front (one memory latency) ----
+  const int pl = t >> 2, qq = t & 3;                          // scores: key row, quarter of hd
+  const int prow = c * CH + (pl < plim ? pl : plim - 1);      // clamped, no branch around the load
+  const uint4* kr = reinterpret_cast<const uint4*>(a.k + kvbase + (size_t)prow * HD + qq * 32);
+  uint4 kv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) kv[i] = kr[i];
+  const int dp = lane * 2, ph = wave;                          // P.V: dim pair, position phase
+  uint32_t vv[CH / 4];
+#pragma unroll
+  for (int j = 0; j < CH / 4; ++j) {
+    const int p = ph + 4 * j;
+    const int pc = c * CH + (p < plim ? p : plim - 1);
+    vv[j] = *reinterpret_cast<const uint32_t*>(a.v + kvbase + (size_t)pc * HD + dp);
+  }
   for (int e = t; e < G * HD / 2; e += 256) {
     const int g = e / (HD / 2), d = (e % (HD / 2)) * 2;
     const uint32_t v = *reinterpret_cast<const uint32_t*>(a.q + (size_t)qi * a.ldq + (kh * G + g) * HD + d);
@@ -58,26 +74,20 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   }
   __syncthreads();
 
-  // ---- scores: thread -> (key row p, quarter of the head dim) ----
+  // ---- scores ----
   {
-    const int pl = t >> 2, qq = t & 3;
-    const int p = c * CH + pl;
     float dot[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) dot[g] = 0.f;
-    if (p <= pos) {
-      const uint4* kr = reinterpret_cast<const uint4*>(a.k + kvbase + (size_t)p * HD + qq * 32);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 kv = kr[i];
-        const uint32_t u[4] = {kv.x, kv.y, kv.z, kv.w};
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u[4] = {kv[i].x, kv[i].y, kv[i].z, kv[i].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float k0 = bf2f(u[j]), k1 = bf2f(u[j] >> 16);
-          const int d = qq * 32 + i * 8 + j * 2;
+      for (int j = 0; j < 4; ++j) {
+        const float k0 = bf2f(u[j]), k1 = bf2f(u[j] >> 16);
+        const int d = qq * 32 + i * 8 + j * 2;
 #pragma unroll
-          for (int g = 0; g < G; ++g) dot[g] += qs[g][d] * k0 + qs[g][d + 1] * k1;
-        }
+        for (int g = 0; g < G; ++g) dot[g] += qs[g][d] * k0 + qs[g][d + 1] * k1;
       }
     }
 #pragma unroll
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
     }
     if (qq == 0) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) sc[g][pl] = (p <= pos) ? dot[g] * a.scale : -INFINITY;
+      for (int g = 0; g < G; ++g) sc[g][pl] = (pl < plim) ? dot[g] * a.scale : -INFINITY;
     }
   }
   __syncthreads();
@@ -106,20 +116,19 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   }
   __syncthreads();
 
-  // ---- P.V: thread -> (dim pair, position phase) ----
+  // ---- P.V (probabilities of clamped padding rows are 0) ----
   {
-    const int dp = lane * 2, ph = wave;
     float o0[G], o1[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) o0[g] = o1[g] = 0.f;
-    const int plim = min(CH, pos - c * CH + 1);
-    for (int pl = ph; pl < plim; pl += 4) {
-      const uint32_t vv = *reinterpret_cast<const uint32_t*>(a.v + kvbase + (size_t)(c * CH + pl) * HD + dp);
-      const float v0 = bf2f(vv), v1 = bf2f(vv >> 16);
+#pragma unroll
+    for (int j = 0; j < CH / 4; ++j) {
+      const int p = ph + 4 * j;
+      const float v0 = bf2f(vv[j]), v1 = bf2f(vv[j] >> 16);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        o0[g] += sc[g][pl] * v0;
-        o1[g] += sc[g][pl] * v1;
+        o0[g] += sc[g][p] * v0;
+        o1[g] += sc[g][p] * v1;
       }
     }
 #pragma unroll

@@ -55,7 +55,7 @@ extern "C" int zmi_graph_end(void* stream, void** graph_exec) {
   ZMI_CHECK(hipStreamEndCapture((hipStream_t)stream, &g));
   hipGraphExec_t ge;
   hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
+  (void)hipGraphDestroy(g);
   ZMI_CHECK(e);
   *graph_exec = (void*)ge;
   return 0;
