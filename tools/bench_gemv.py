@@ -1,0 +1,71 @@
+"""Micro-benchmark of the decode GEMV shapes (M = 2 rows) over split-K choices, HIP-event timed.
+
+Weights are rotated over `copies` distinct buffers (> 256 MiB in total) so each launch streams
+from HBM, as in the decode step. Prints one JSON line per (shape, ksplit).
+"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zonos_vibes_amd import _lib  # noqa: E402
+
+L = _lib.lib()
+dev = "cuda"
+SHAPES = {  # name: (N, K, epi, ln)
+    "qkv": (3072, 2048, _lib.EPI_STORE, True),
+    "out": (2048, 2048, _lib.EPI_RESIDUAL, False),
+    "fc1": (16384, 2048, _lib.EPI_SWIGLU, True),
+    "fc2": (2048, 8192, _lib.EPI_RESIDUAL, False),
+    "heads": (9248, 2048, _lib.EPI_STORE, True),
+}
+
+
+def run(name, M=2, reps=20, ksplits=(1, 2, 4, 8)):
+    N, K, epi, ln = SHAPES[name]
+    wbytes = N * K * 2
+    copies = max(2, (400 << 20) // wbytes + 1)
+    Ws = [torch.randn(N * K, device=dev).to(torch.bfloat16) for _ in range(copies)]
+    X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    out = torch.zeros(M, max(N, K), device=dev).to(torch.bfloat16)
+    lw, lb = torch.ones(K, device=dev).to(torch.bfloat16), torch.zeros(K, device=dev).to(torch.bfloat16)
+    slab = torch.zeros(M * N * 16 + 16, device=dev)
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for ks in ksplits:
+        if (K // 32) % (4 * ks):
+            continue
+        args = []
+        for W in Ws:
+            a = _lib.GemvArgs()
+            a.W, a.X, a.M, a.N, a.K, a.ldx = W.data_ptr(), X.data_ptr(), M, N, K, K
+            a.ksplit = ks
+            if ln:
+                a.ln_w, a.ln_b, a.eps = lw.data_ptr(), lb.data_ptr(), 1e-5
+            a.out, a.ldo, a.n_valid = out.data_ptr(), (N // 2 if epi == _lib.EPI_SWIGLU else N), N
+            a.slab, a.counters = slab.data_ptr(), cnt.data_ptr()
+            args.append(a)
+        for a in args:
+            _lib.check(L.zmi_gemv_launch(ctypes.byref(a), epi, s))
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(reps):
+            for a in args:
+                L.zmi_gemv_launch(ctypes.byref(a), epi, s)
+        en.record()
+        en.synchronize()
+        us = st.elapsed_time(en) * 1e3 / (reps * len(args))
+        r = dict(shape=name, N=N, K=K, M=M, ksplit=ks, us=round(us, 2), GBps=round(wbytes / us / 1e3, 1))
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    return res
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(SHAPES)
+    for n in names:
+        run(n)

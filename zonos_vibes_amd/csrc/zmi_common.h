@@ -80,7 +80,30 @@ __device__ __forceinline__ bool zmi_last_arriver(unsigned* counter, unsigned tot
   return *lds_flag != 0;
 }
 
-#define ZMI_CHECK(expr)                                                     \
+// Write-through variant (MI355X_MICROARCH.md "Valid forms", table row 1): every byte handed off is
+// stored with an agent-scope relaxed atomic store (global_store ... sc1, drained by vmcnt(0) in every
+// storing wave before the barrier), one lane bumps the ticket; the last arriver reads the slabs
+// with agent-scope relaxed loads (sc1). No release/acquire fences, no L2 write-back.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool zmi_last_arriver_wt(unsigned* counter, unsigned total, unsigned* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = (t == total - 1) ? 1u : 0u;
+    if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+#define ZMI_CHECK(expr)                                                   \
   do {                                                                      \
     hipError_t _e = (expr);                                                 \
     if (_e != hipSuccess) return zmi_fail(_e, #expr, __FILE__, __LINE__);   \

@@ -9,13 +9,26 @@ namespace zmi_gemv {
 
 constexpr int PRO_PLAIN = 0, PRO_LN = 1;
 
+template <int MT>
+struct GemvLds {
+  static constexpr int RED = 0;
+  static constexpr int TILE = RED + 4 * MT * 64 * 4 * 4;
+  static constexpr int LN = TILE + MT * 16 * 17 * 4;
+  static constexpr int FLAG = LN + 2 * MT * 16 * 4;
+  static constexpr int XS = FLAG + 16;
+};
+
 template <int MT, int NF, int PRO, int EPI, bool XLDS>
 __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // XLDS: activation rows [rows][ldx_s]
-  __shared__ float red[4][MT][64][4];
-  __shared__ float tile[MT * 16][17];
-  __shared__ float ln_mean[MT * 16], ln_rstd[MT * 16];
-  __shared__ unsigned last_flag;
+  // all LDS in one dynamic block, carved at 16 B multiples (no static __shared__ shifting the base:
+  // cdna_hip_programming.md §6 Guideline 17)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float(&red)[4][MT][64][4] = *reinterpret_cast<float(*)[4][MT][64][4]>(smem);
+  float(&tile)[MT * 16][17] = *reinterpret_cast<float(*)[MT * 16][17]>(smem + GemvLds<MT>::TILE);
+  float* ln_mean = reinterpret_cast<float*>(smem + GemvLds<MT>::LN);
+  float* ln_rstd = ln_mean + MT * 16;
+  unsigned& last_flag = *reinterpret_cast<unsigned*>(smem + GemvLds<MT>::FLAG);
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem + GemvLds<MT>::XS);  // XLDS: activation rows [rows][ldx_s]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int NT = a.N >> 4, KT = a.K >> 5;
@@ -35,18 +48,40 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   const u32x4_t* wbase = reinterpret_cast<const u32x4_t*>(a.W) + ((size_t)nt * KT + kt_base) * 64 + lane;
   const int arow = lane & 15, kq = (lane >> 4) * 8;
 
-  // (1) the weight stream does not depend on the activations: issue chunk 0 first
-  u32x4_t wf[NF];
-#pragma unroll
-  for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(wave * NF + f) * 64);
-
-  // (2) activations -> LDS (XLDS), LayerNorm statistics
+  // (1) activation rows first (they gate the LayerNorm): up to 4 x 16 B per thread into registers,
+  //     unconditional loads from clamped addresses (no branch -> no vmcnt(0) per load)
   const int xw = (PRO == PRO_LN) ? a.K : KB;          // columns staged per row
   const int xk0 = (PRO == PRO_LN) ? 0 : kb0;          // first staged column
   const int ldx_s = xw + 8;
+  const int per_row = xw >> 3, n_x = rows * per_row;
+  uint4 xr[4];
   if (XLDS) {
-    const int per_row = xw >> 3;
-    for (int e = threadIdx.x; e < rows * per_row; e += 256) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int e = threadIdx.x + i * 256;
+      e = e < n_x ? e : n_x - 1;
+      const int r = e / per_row, c = (e - r * per_row) * 8;
+      xr[i] = *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + xk0 + c);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the activation loads ahead of the weight stream
+  // (2) the weight stream does not depend on the activations: issue chunk 0 right away
+  u32x4_t wf[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(wave * NF + f) * 64);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // (3) registers -> LDS while the weights are in flight; LayerNorm statistics
+  if (XLDS) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < n_x) {
+        const int r = e / per_row, c = (e - r * per_row) * 8;
+        *reinterpret_cast<uint4*>(xs + r * ldx_s + c) = xr[i];
+      }
+    }
+    for (int e = threadIdx.x + 1024; e < n_x; e += 256) {
       const int r = e / per_row, c = (e - r * per_row) * 8;
       *reinterpret_cast<uint4*>(xs + r * ldx_s + c) =
           *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + xk0 + c);
@@ -75,9 +110,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
           ss += d0 * d0 + d1 * d1;
         }
       }
+      const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)a.K + a.eps);  // all lanes: wave reduction
       if (lane == 0) {
         ln_mean[r] = mean;
-        ln_rstd[r] = 1.0f / sqrtf(wave_sum(ss) / (float)a.K + a.eps);
+        ln_rstd[r] = rstd;
       }
     }
     __syncthreads();
@@ -167,11 +203,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   if (a.ksplit > 1) {
     const size_t tid = (size_t)blockIdx.y * NT + nt;
     float* slab = a.slab + tid * (size_t)a.ksplit * (MT * 256);
-    for (int e = threadIdx.x; e < rows * 16; e += 256) slab[(size_t)ks * (MT * 256) + e] = tile[e >> 4][e & 15];
-    if (!zmi_last_arriver(a.counters + tid, (unsigned)a.ksplit, &last_flag)) return;
+    for (int e = threadIdx.x; e < rows * 16; e += 256) st_wt(slab + (size_t)ks * (MT * 256) + e, tile[e >> 4][e & 15]);
+    if (!zmi_last_arriver_wt(a.counters + tid, (unsigned)a.ksplit, &last_flag)) return;
     for (int e = threadIdx.x; e < rows * 16; e += 256) {
-      float v = slab[e];
-      for (int s = 1; s < a.ksplit; ++s) v += slab[(size_t)s * (MT * 256) + e];
+      float v = ld_wt(slab + e);
+      for (int s = 1; s < a.ksplit; ++s) v += ld_wt(slab + (size_t)s * (MT * 256) + e);
       tile[e >> 4][e & 15] = v;
     }
     __syncthreads();
@@ -253,9 +289,9 @@ hipError_t launch_t(const ZmiGemvArgs& a, hipStream_t s) {
   const int xw = PRO == PRO_LN ? a.K : a.K / a.ksplit;
   const size_t lds = (size_t)rows * (xw + 8) * sizeof(bf16_t);
   if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, true>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, true>), grid, dim3(256), GemvLds<MT>::XS + lds, s, a);
   else
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, false>), grid, dim3(256), GemvLds<MT>::XS, s, a);
   return hipGetLastError();
 }
 
