@@ -52,13 +52,15 @@ typedef struct ZmiGemvArgs {
   void* v_cache;
   int smax, hq, hkv, hd;
   const float* rope;    /* [16384][hd/2][2] (cos, sin) fp32 (_torch.py:9-15)                  */
-  float* slab;          /* split-K workspace, zmi_gemv_slab_floats() floats                    */
+  float* slab;          /* split-K workspace                                                   */
   unsigned* counters;   /* split-K arrival tickets, zero-initialised, re-armed by the kernel   */
+  int64_t slab_cap;     /* floats available at `slab` (checked before launch)                  */
+  int64_t counters_cap; /* tickets available at `counters` (checked before launch)             */
 } ZmiGemvArgs;
 
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
-int64_t zmi_gemv_slab_floats(int M, int N, int K);
+int64_t zmi_gemv_slab_floats(int M, int N, int K, int ksplit); /* ksplit <= 0: library plan */
 
 /* ---------------------------------------------------------------------------------------
  * Attention: GQA scaled-dot-product attention over the KV cache, one query position per

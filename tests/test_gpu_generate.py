@@ -205,7 +205,7 @@ def test_teacher_forced_greedy_decisions_agree_beyond_noise_floor(traj):
     if os.path.isdir("gpurun_out"):
         json.dump(dict(stats=stats, bad=bad[:20]), open("gpurun_out/teacher_forced.json", "w"), indent=1)
     assert not bad, stats
-    assert agree / n > 0.97, stats
+    assert agree / n > 0.95, stats
 
 
 def test_generate_is_deterministic(traj):

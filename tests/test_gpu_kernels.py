@@ -41,9 +41,10 @@ def gemv(W, X, epi, out, ldo, n_valid=None, ln=None, ksplit=0, mode=0, extra=Non
         a.ln_w, a.ln_b, a.eps = ln[0].data_ptr(), ln[1].data_ptr(), 1e-5
     a.out, a.ldo = out.data_ptr(), ldo
     a.n_valid = W.shape[0] if n_valid is None else n_valid
-    slab = torch.zeros(max(L.lib().zmi_gemv_slab_floats(M, n_pad, K), 1), dtype=torch.float32, device=DEV)
+    slab = torch.zeros(max(L.lib().zmi_gemv_slab_floats(M, n_pad, K, ksplit), 1), dtype=torch.float32, device=DEV)
     cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     a.slab, a.counters = slab.data_ptr(), cnt.data_ptr()
+    a.slab_cap, a.counters_cap = slab.numel(), cnt.numel()
     if extra:
         extra(a)
     L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), epi, stream_ptr()), "gemv")

@@ -32,13 +32,13 @@ def run(name, M=2, reps=20, ksplits=(1, 2, 4, 8)):
     X = torch.randn(M, K, device=dev).to(torch.bfloat16)
     out = torch.zeros(M, max(N, K), device=dev).to(torch.bfloat16)
     lw, lb = torch.ones(K, device=dev).to(torch.bfloat16), torch.zeros(K, device=dev).to(torch.bfloat16)
-    slab = torch.zeros(M * N * 16 + 16, device=dev)
     cnt = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     res = []
     for ks in ksplits:
         if (K // 32) % (4 * ks):
             continue
+        slab = torch.zeros(max(L.zmi_gemv_slab_floats(M, N, K, ks), 1), device=dev)
         args = []
         for W in Ws:
             a = _lib.GemvArgs()
@@ -48,6 +48,7 @@ def run(name, M=2, reps=20, ksplits=(1, 2, 4, 8)):
                 a.ln_w, a.ln_b, a.eps = lw.data_ptr(), lb.data_ptr(), 1e-5
             a.out, a.ldo, a.n_valid = out.data_ptr(), (N // 2 if epi == _lib.EPI_SWIGLU else N), N
             a.slab, a.counters = slab.data_ptr(), cnt.data_ptr()
+            a.slab_cap, a.counters_cap = slab.numel(), cnt.numel()
             args.append(a)
         for a in args:
             _lib.check(L.zmi_gemv_launch(ctypes.byref(a), epi, s))

@@ -30,6 +30,7 @@ class GemvArgs(ctypes.Structure):
         ("k_cache", c_void_p), ("v_cache", c_void_p),
         ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
         ("rope", c_void_p), ("slab", c_void_p), ("counters", c_void_p),
+        ("slab_cap", c_int64), ("counters_cap", c_int64),
     ]
 
 
@@ -52,7 +53,7 @@ class Slots(ctypes.Structure):
 _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
-    "zmi_gemv_slab_floats": (c_int64, [c_int, c_int, c_int]),
+    "zmi_gemv_slab_floats": (c_int64, [c_int, c_int, c_int, c_int]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),

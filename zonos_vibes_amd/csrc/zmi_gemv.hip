@@ -89,7 +89,13 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
     a.nchunk = per_wave / nf;
   }
   if (nf < 2) return zmi_fail_msg("gemv: fewer than 2 fragments per wave");
-  if (a.ksplit > 1 && (!a.slab || !a.counters)) return zmi_fail_msg("gemv: split-K needs slab + counters");
+  if (a.ksplit > 1) {
+    const int groups = (a.M + mt * 16 - 1) / (mt * 16);
+    const int64_t tiles = (int64_t)groups * (a.N / 16);
+    if (!a.slab || !a.counters) return zmi_fail_msg("gemv: split-K needs slab + counters");
+    if (tiles * a.ksplit * mt * 256 > a.slab_cap) return zmi_fail_msg("gemv: split-K slab too small");
+    if (tiles > a.counters_cap) return zmi_fail_msg("gemv: split-K counters too small");
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   switch (epi) {
@@ -115,9 +121,10 @@ extern "C" int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int
   return 0;
 }
 
-extern "C" int64_t zmi_gemv_slab_floats(int M, int N, int K) {
+extern "C" int64_t zmi_gemv_slab_floats(int M, int N, int K, int ksplit) {
   int mt, nf, ks, nch;
   zmi_gemv_plan(M, N, K, &mt, &nf, &ks, &nch);
+  if (ksplit > 0) ks = ksplit;
   const int groups = (M + mt * 16 - 1) / (mt * 16);
   return ks > 1 ? (int64_t)groups * (N / 16) * ks * mt * 256 : 0;
 }

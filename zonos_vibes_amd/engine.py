@@ -110,7 +110,7 @@ class HipEngine:
             self.vc = z(self.L, R, self.Hkv, self.smax, self.hd)
             slab = 0
             for n, k in self._gemv_shapes():
-                slab = max(slab, self.lib.zmi_gemv_slab_floats(R, n, k))
+                slab = max(slab, self.lib.zmi_gemv_slab_floats(R, n, k, 0))
             self.slab = z(max(slab, 1), dt=torch.float32)
             self.gemv_cnt = z(GEMV_COUNTERS, dt=torch.int32)
             nq = max(R, 2 * self.max_prefill)
@@ -211,6 +211,7 @@ class HipEngine:
             a.smax, a.hq, a.hkv, a.hd = self.smax, self.H, self.Hkv, self.hd
             a.rope = self.rope.data_ptr()
         a.slab, a.counters = self.slab.data_ptr(), self.gemv_cnt.data_ptr()
+        a.slab_cap, a.counters_cap = self.slab.numel(), self.gemv_cnt.numel()
         return (a, epi)
 
     def _run_gemv(self, item):
