@@ -84,9 +84,15 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
   } else {
     const int per_wave = (a.K / 32) / (a.ksplit * 4);
     if (per_wave * a.ksplit * 4 != a.K / 32) return zmi_fail_msg("gemv: K/32 not divisible by 4*ksplit");
-    nf = per_wave >= 16 ? 16 : (per_wave >= 8 ? 8 : (per_wave >= 4 ? 4 : 2));
-    while (per_wave % nf) nf >>= 1;
-    a.nchunk = per_wave / nf;
+    if (a.nchunk > 0) {  // caller-chosen chunking (tuning): NF = per_wave / nchunk
+      if (per_wave % a.nchunk) return zmi_fail_msg("gemv: nchunk must divide the fragments per wave");
+      nf = per_wave / a.nchunk;
+      if (nf != 2 && nf != 4 && nf != 8 && nf != 16) return zmi_fail_msg("gemv: fragments per chunk not in {2,4,8,16}");
+    } else {
+      nf = per_wave >= 16 ? 16 : (per_wave >= 8 ? 8 : (per_wave >= 4 ? 4 : 2));
+      while (per_wave % nf) nf >>= 1;
+      a.nchunk = per_wave / nf;
+    }
   }
   if (nf < 2) return zmi_fail_msg("gemv: fewer than 2 fragments per wave");
   if (a.ksplit > 1) {

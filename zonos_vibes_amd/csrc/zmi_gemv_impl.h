@@ -8,6 +8,7 @@ namespace zmi_gemv {
 
 
 constexpr int PRO_PLAIN = 0, PRO_LN = 1;
+constexpr int XS_GLOBAL = 0, XS_REG = 1, XS_DMA = 2;  // where the A-operand rows come from
 
 template <int MT>
 struct GemvLds {
@@ -18,7 +19,7 @@ struct GemvLds {
   static constexpr int XS = FLAG + 16;
 };
 
-template <int MT, int NF, int PRO, int EPI, bool XLDS>
+template <int MT, int NF, int PRO, int EPI, int XLDS>
 __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   // all LDS in one dynamic block, carved at 16 B multiples (no static __shared__ shifting the base:
   // cdna_hip_programming.md §6 Guideline 17)
@@ -55,7 +56,37 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   const int ldx_s = xw + 8;
   const int per_row = xw >> 3, n_x = rows * per_row;
   uint4 xr[4];
-  if (XLDS) {
+  if (XLDS == XS_DMA) {
+    // 1 KiB LDS-DMA pieces (64 lanes x 16 B, lane-linear, never crossing a row): no VGPRs, so the
+    // weight stream below is not held back by register reuse
+    // Issued as inline asm: the compiler then does not treat the in-flight DMA as a pending LDS
+    // write and does not drain the whole vm queue (the weights) before the first ds_read; the
+    // covering wait is the explicit vmcnt(NF) below (cdna_hip_programming.md §5.7).
+    // pieces: activation rows, then (LayerNorm) gamma and beta of this block's k-range
+    const int ppr = xw >> 9, n_x_pc = rows * ppr, ppk = KB >> 9;
+    const int n_pc = n_x_pc + (PRO == PRO_LN ? 2 * ppk : 0);
+    for (int pc = wave; pc < n_pc; pc += 4) {
+      const bf16_t* gsrc;
+      bf16_t* ldp;
+      if (pc < n_x_pc) {
+        const int r = pc / ppr, p = pc - r * ppr;
+        gsrc = X + (size_t)(row0 + r) * a.ldx + xk0 + p * 512 + lane * 8;
+        ldp = xs + r * ldx_s + p * 512;
+      } else {
+        const int q = pc - n_x_pc, which = q / ppk, p = q - which * ppk;
+        gsrc = (which ? lnb : lnw) + kb0 + p * 512 + lane * 8;
+        ldp = xs + rows * ldx_s + which * KB + p * 512;
+      }
+      const unsigned ldst = __builtin_amdgcn_readfirstlane(
+          (unsigned)(size_t)(__attribute__((address_space(3))) void*)ldp);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(gsrc), "s"(ldst)
+                   : "memory");
+    }
+  } else if (XLDS == XS_REG) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int e = threadIdx.x + i * 256;
@@ -71,8 +102,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(wave * NF + f) * 64);
   __builtin_amdgcn_sched_barrier(0);
 
-  // (3) registers -> LDS while the weights are in flight; LayerNorm statistics
-  if (XLDS) {
+  // (3) activations visible in LDS while the weights are still in flight; LayerNorm statistics
+  if (XLDS == XS_DMA) {
+    // this wave's DMA pieces are older than its NF weight loads; a raw barrier (no vmcnt(0) drain)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else if (XLDS == XS_REG) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = threadIdx.x + i * 256;
@@ -122,7 +158,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
       for (int e = threadIdx.x; e < rows * per_row; e += 256) {
         const int r = e / per_row, c = kb0 + (e - r * per_row) * 8;
         uint4* p = reinterpret_cast<uint4*>(xs + r * ldx_s + c);
-        const uint4 v = *p, gw = *reinterpret_cast<const uint4*>(lnw + c), gb = *reinterpret_cast<const uint4*>(lnb + c);
+        uint4 gw, gb;
+        if (XLDS == XS_DMA) {  // gamma / beta were DMA'd next to the rows
+          gw = *reinterpret_cast<const uint4*>(xs + rows * ldx_s + (c - kb0));
+          gb = *reinterpret_cast<const uint4*>(xs + rows * ldx_s + KB + (c - kb0));
+        } else {
+          gw = *reinterpret_cast<const uint4*>(lnw + c);
+          gb = *reinterpret_cast<const uint4*>(lnb + c);
+        }
+        const uint4 v = *p;
         const float rstd = ln_rstd[r], nbias = -ln_mean[r] * rstd;
         uint32_t u[4] = {v.x, v.y, v.z, v.w};
         const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
@@ -287,11 +331,15 @@ hipError_t launch_t(const ZmiGemvArgs& a, hipStream_t s) {
   // stage the activation rows in LDS when they fit (always for decode-sized M)
   const int rows = a.M < MT * 16 ? a.M : MT * 16;
   const int xw = PRO == PRO_LN ? a.K : a.K / a.ksplit;
+  const int kb = a.K / a.ksplit;
   const size_t lds = (size_t)rows * (xw + 8) * sizeof(bf16_t);
-  if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, true>), grid, dim3(256), GemvLds<MT>::XS + lds, s, a);
+  const size_t lds_dma = lds + (PRO == PRO_LN ? 2 * (size_t)kb * sizeof(bf16_t) : 0);
+  if (lds_dma <= 64 * 1024 && xw % 512 == 0 && kb % 512 == 0)
+    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_DMA>), grid, dim3(256), GemvLds<MT>::XS + lds_dma, s, a);
+  else if (lds <= 64 * 1024)
+    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_REG>), grid, dim3(256), GemvLds<MT>::XS + lds, s, a);
   else
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, false>), grid, dim3(256), GemvLds<MT>::XS, s, a);
+    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_GLOBAL>), grid, dim3(256), GemvLds<MT>::XS, s, a);
   return hipGetLastError();
 }
 
