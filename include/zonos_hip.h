@@ -98,9 +98,12 @@ typedef struct ZmiSlots {
   int n_slots;
 } ZmiSlots;
 
-/* mode 0 = decode step (bias + penalty + FSM), 1 = prefill (no bias, no penalty, no FSM) */
+/* mode 0 = decode step (bias + penalty + FSM), 1 = prefill (no bias, no penalty, no FSM).
+ * With emb != NULL the slot's next input frame is embedded in the same launch (x[2s], x[2s+1],
+ * model.py:97-98,142) and row_kv/row_pos (optional) receive the next step's KV row / position. */
 int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
-                    unsigned* counters, int mode, int slot_begin, int slot_count, void* stream);
+                    unsigned* counters, int mode, int slot_begin, int slot_count, const void* emb, int d, void* x,
+                    int* row_kv, int* row_pos, void* stream);
 /* x[2s], x[2s+1] = sum_k emb_k[delayed[s][k][offset[s]]]  (model.py:97-98,142) and the
  * per-row (kv row, position) tables of the step (-1 position for inactive slots). */
 int zmi_embed_step(const ZmiSlots* slots, const void* emb, int d, void* x, int* row_kv, int* row_pos,

@@ -114,6 +114,7 @@ def test_full_width_layer_logits_match_reference():
         with torch.cuda.stream(e.stream):
             e.delayed[0, :, o] = t["feed"][s].reshape(9).to(DEV, torch.int32)
             e.st["remaining"][0] = 100
+            e.refresh_inputs()
         e.step(1, use_graph=False)
         e.stream.synchronize()
         check(cfg_logits(e.logits[0:2]), t["step_logits"][s])
@@ -154,6 +155,7 @@ def _teacher_forced(cfg, model_kw, cond, n, seed=0):
     scores = [None]
     with torch.cuda.stream(e.stream):
         e.delayed[0, :, :delayed.shape[-1]] = delayed.to(DEV, torch.int32)
+        e.refresh_inputs()
     for s in range(n + 8):
         o = int(e.st["offset"][0].item())
         e.step(1, use_graph=False)

@@ -209,7 +209,8 @@ def _run_sampler_on_final_logits(logits, generated, sp, noise=None):
     cnt = torch.zeros(B, dtype=torch.int32, device=DEV)
     nz = None if noise is None else noise.to(DEV).contiguous()
     L.check(L.lib().zmi_sample_step(ctypes.byref(sl), rows.data_ptr(), None if nz is None else nz.data_ptr(),
-                                    nxt.data_ptr(), cnt.data_ptr(), 0, 0, B, stream_ptr()))
+                                    nxt.data_ptr(), cnt.data_ptr(), 0, 0, B, None, 0, None, None, None,
+                                    stream_ptr()))
     torch.cuda.synchronize()
     return nxt.cpu().long().unsqueeze(-1), st, delayed
 

@@ -58,7 +58,7 @@ _SIGS = {
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                                c_void_p]),
+                                c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_codes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "zmi_delay_init": (c_int, [ctypes.POINTER(Slots), c_int, c_void_p, c_int, c_int, c_void_p]),

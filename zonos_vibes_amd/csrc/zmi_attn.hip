@@ -155,27 +155,28 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   // ---- publish chunk partial; last chunk merges in chunk order ----
   const size_t pstride = (size_t)G * (HD + 2);
   float* base = a.part + (size_t)blockIdx.x * a.maxch * pstride;
+  // write-through (sc1) stores + ticket; the last chunk reads every partial with sc1 loads
   for (int e = t; e < G * HD; e += 256) {
     const int g = e / HD, d = e % HD;
-    base[c * pstride + g * (HD + 2) + 2 + d] =
-        ((opart[0][g][d] + opart[1][g][d]) + opart[2][g][d]) + opart[3][g][d];
+    st_wt(base + c * pstride + g * (HD + 2) + 2 + d,
+          ((opart[0][g][d] + opart[1][g][d]) + opart[2][g][d]) + opart[3][g][d]);
   }
   if (t < G) {
-    base[c * pstride + t * (HD + 2)] = mlv[t][0];
-    base[c * pstride + t * (HD + 2) + 1] = mlv[t][1];
+    st_wt(base + c * pstride + t * (HD + 2), mlv[t][0]);
+    st_wt(base + c * pstride + t * (HD + 2) + 1, mlv[t][1]);
   }
-  if (!zmi_last_arriver(a.counters + blockIdx.x, (unsigned)nch, &last_flag)) return;
+  if (!zmi_last_arriver_wt(a.counters + blockIdx.x, (unsigned)nch, &last_flag)) return;
 
   float mmax = -INFINITY;
-  for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, base[cc * pstride + g_t * (HD + 2)]);
+  for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, ld_wt(base + cc * pstride + g_t * (HD + 2)));
   float L = 0.f;
   float o[HD / (256 / G) > 0 ? HD / (256 / G) : 1];
   for (int i = 0; i < nd; ++i) o[i] = 0.f;
   for (int cc = 0; cc < nch; ++cc) {
     const float* pc = base + cc * pstride + g_t * (HD + 2);
-    const float w = expf(pc[0] - mmax);
-    L += w * pc[1];
-    for (int i = 0; i < nd; ++i) o[i] += w * pc[2 + d_t + i];
+    const float w = expf(ld_wt(pc) - mmax);
+    L += w * ld_wt(pc + 1);
+    for (int i = 0; i < nd; ++i) o[i] += w * ld_wt(pc + 2 + d_t + i);
   }
   const float inv_l = 1.0f / L;
   for (int i = 0; i < nd; ++i)

@@ -60,13 +60,16 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, uint4* __restrict__ 
 void zmi_gemv_plan(int M, int N, int K, int* mt, int* nf, int* ksplit, int* nchunk) {
   const int KT = K / 32;
   int m = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
-  // target >= ~512 blocks for the HBM stream; fragments per wave <= 16
+  // Measured on MI355X (tools/bench_gemv.py, M = 2): split-K never pays at the decode shapes
+  // (the extra hand-off and per-block activation staging cost more than the added parallelism),
+  // so every block owns a full K column strip. Grids with >= 512 strips run 8 fragments per
+  // chunk (lower VGPR use), smaller grids 16.
   const int nt = N / 16;
-  int ks = 1;
-  while (nt * ks < 512 && (KT % (ks * 2 * 4)) == 0 && KT / (ks * 2 * 4) >= 4) ks *= 2;
-  int per_wave = KT / (ks * 4);
-  int f = per_wave >= 16 ? 16 : (per_wave >= 8 ? 8 : (per_wave >= 4 ? 4 : 2));
-  while (per_wave % f) f >>= 1;
+  const int ks = 1;
+  const int per_wave = KT / 4;
+  int f = (nt >= 512 ? 8 : 16);
+  while (f > per_wave) f >>= 1;
+  while (f > 2 && per_wave % f) f >>= 1;
   *mt = m;
   *nf = f;
   *ksplit = ks;

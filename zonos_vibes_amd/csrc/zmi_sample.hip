@@ -27,7 +27,14 @@ struct SampleArgs {
   unsigned* counters;
   int mode;
   int slot_begin;
+  const bf16_t* emb;  // optional fused embedding of the next input frame
+  int d;
+  bf16_t* x;
+  int* row_kv;
+  int* row_pos;
 };
+
+__device__ void embed_row(const int* toks, const bf16_t* emb, int d, bf16_t* out0, bf16_t* out1);
 
 __device__ float block_reduce_sum(float v, float* red) {
   v = wave_sum(v);
@@ -271,46 +278,66 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     tok = block_argmax(bv, bi, redv, redi);
   }
 
-  if (t == 0) a.next[(size_t)s * ZMI_NCB + cb] = tok;
-  if (!zmi_last_arriver(a.counters + s, ZMI_NCB, &last_flag)) return;
+  if (t == 0) st_wt(a.next + (size_t)s * ZMI_NCB + cb, tok);
+  if (!zmi_last_arriver_wt(a.counters + s, ZMI_NCB, &last_flag)) return;
 
-  // ---- EOS state machine + frame compaction write (one thread per slot) ----
-  if (t != 0) return;
-  int nt[ZMI_NCB];
-  for (int k = 0; k < ZMI_NCB; ++k) nt[k] = a.next[(size_t)s * ZMI_NCB + k];
-  int rem = a.sl.remaining[s];
-  int stop = a.sl.stopping[s];
-  if (decode) {
-    if (nt[0] == ZMI_EOS) {
-      rem = min(rem, 9);
-      stop = 1;
+  // ---- EOS state machine + frame compaction write (thread 0 of the slot's last block) ----
+  __shared__ int frame[ZMI_NCB + 2];
+  if (t == 0) {
+    int nt[ZMI_NCB];
+    for (int k = 0; k < ZMI_NCB; ++k) nt[k] = ld_wt(a.next + (size_t)s * ZMI_NCB + k);
+    int rem = a.sl.remaining[s];
+    int stop = a.sl.stopping[s];
+    if (decode) {
+      if (nt[0] == ZMI_EOS) {
+        rem = min(rem, 9);
+        stop = 1;
+      }
+      if (stop) {
+        const int idx = min(9 - rem, 8);
+        for (int k = 0; k < idx; ++k) nt[k] = ZMI_MASK;
+        nt[idx] = ZMI_EOS;
+      }
     }
-    if (stop) {
-      const int idx = min(9 - rem, 8);
-      for (int k = 0; k < idx; ++k) nt[k] = ZMI_MASK;
-      nt[idx] = ZMI_EOS;
-    }
-  }
-  if (o < a.sl.total_len[s]) {
     int kk = 0;
     for (int k = 0; k < ZMI_NCB; ++k) {
       int* cell = a.sl.delayed + ((size_t)s * ZMI_NCB + k) * a.sl.tcap + o;
-      if (*cell == -1) *cell = nt[kk++];
+      int v = o < a.sl.total_len[s] ? *cell : ZMI_MASK;
+      if (o < a.sl.total_len[s] && v == -1) *cell = v = nt[kk++];
+      frame[k] = v < 0 ? 0 : (v > ZMI_MASK ? ZMI_MASK : v);  // next step's input frame
+    }
+    a.sl.offset[s] = o;
+    int pos = a.sl.pos[s], act = 1;
+    if (decode) {
+      pos += 1;
+      a.sl.pos[s] = pos;
+      rem -= 1;
+      a.sl.remaining[s] = rem;
+      a.sl.stopping[s] = stop;
+      a.sl.step[s] += 1;
+      if (rem <= 0) {
+        a.sl.active[s] = 0;
+        act = 0;
+      }
+    }
+    frame[ZMI_NCB] = act;
+    if (a.row_pos) {  // (kv row, position) of the next step's CFG pair
+      a.row_kv[2 * s] = 2 * s;
+      a.row_kv[2 * s + 1] = 2 * s + 1;
+      a.row_pos[2 * s] = act ? pos : -1;
+      a.row_pos[2 * s + 1] = act ? pos : -1;
     }
   }
-  a.sl.offset[s] = o;
-  if (decode) {
-    a.sl.pos[s] += 1;
-    rem -= 1;
-    a.sl.remaining[s] = rem;
-    a.sl.stopping[s] = stop;
-    a.sl.step[s] += 1;
-    if (rem <= 0) a.sl.active[s] = 0;
+  // ---- next step's input embedding: x[2s] = x[2s+1] = sum_k emb_k[frame_k]  (model.py:97-98,142)
+  if (a.emb) {
+    __syncthreads();
+    if (frame[ZMI_NCB])
+      embed_row(frame, a.emb, a.d, a.x + (size_t)(2 * s) * a.d, a.x + (size_t)(2 * s + 1) * a.d);
   }
 }
 
 // ---- embeddings (model.py:97-98): sum over codebooks 0..8, bf16 rounding after each add ----
-__device__ __forceinline__ void embed_row(const int* toks, const bf16_t* emb, int d, bf16_t* out0, bf16_t* out1) {
+__device__ void embed_row(const int* toks, const bf16_t* emb, int d, bf16_t* out0, bf16_t* out1) {
   for (int c = threadIdx.x * 8; c < d; c += 256 * 8) {
     float acc[8];
 #pragma unroll
@@ -389,8 +416,11 @@ __global__ void delay_revert_kernel(const ZmiSlots sl, int slot, int64_t* out, i
 }  // namespace
 
 extern "C" int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
-                               unsigned* counters, int mode, int slot_begin, int slot_count, void* stream) {
+                               unsigned* counters, int mode, int slot_begin, int slot_count, const void* emb, int d,
+                               void* x, int* row_kv, int* row_pos, void* stream) {
   if (slot_begin < 0 || slot_begin + slot_count > slots->n_slots) return zmi_fail_msg("sample: slot range");
+  if (emb && (d % 8 || !x)) return zmi_fail_msg("sample: fused embedding needs x and d % 8 == 0");
+  if (!row_kv != !row_pos) return zmi_fail_msg("sample: row_kv and row_pos go together");
   SampleArgs a;
   a.sl = *slots;
   a.logits = logits_rows;
@@ -399,6 +429,11 @@ extern "C" int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, 
   a.counters = counters;
   a.mode = mode;
   a.slot_begin = slot_begin;
+  a.emb = (const bf16_t*)emb;
+  a.d = d;
+  a.x = (bf16_t*)x;
+  a.row_kv = row_kv;
+  a.row_pos = row_pos;
   hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, slot_count), dim3(256), 0, (hipStream_t)stream, a);
   ZMI_CHECK(hipGetLastError());
   return 0;

@@ -105,7 +105,7 @@ class HipEngine:
             self.h = z(R, self.F)
             self.logits = z(R, N_CODEBOOKS, 1026, dt=torch.float32)
             self.row_kv = z(R, dt=torch.int32)
-            self.row_pos = z(R, dt=torch.int32)
+            self.row_pos = torch.full((R,), -1, dtype=torch.int32, device=dev)  # every row inactive
             self.kc = z(self.L, R, self.Hkv, self.smax, self.hd)
             self.vc = z(self.L, R, self.Hkv, self.smax, self.hd)
             slab = 0
@@ -246,20 +246,32 @@ class HipEngine:
                                           self.smax, max_pos, out.data_ptr(), self.H * self.hd,
                                           self.attn_part.data_ptr(), self.attn_cnt.data_ptr(), self.sptr), "attention")
 
+    def refresh_inputs(self):
+        """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
+        edit of `delayed`, e.g. teacher forcing in tests); normally the sampler produces them."""
+        _lib.check(self.lib.zmi_embed_step(ctypes.byref(self.slots), self.w["emb"].data_ptr(), self.d,
+                                           self.x.data_ptr(), self.row_kv.data_ptr(), self.row_pos.data_ptr(),
+                                           self.sptr), "embed")
+
+    def _sample(self, logits, noise, mode, slot_begin, count):
+        _lib.check(self.lib.zmi_sample_step(ctypes.byref(self.slots), logits.data_ptr(),
+                                            None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
+                                            self.samp_cnt.data_ptr(), mode, slot_begin, count,
+                                            self.w["emb"].data_ptr(), self.d, self.x.data_ptr(),
+                                            self.row_kv.data_ptr(), self.row_pos.data_ptr(), self.sptr), "sample")
+
     def enqueue_step(self, noise: torch.Tensor | None = None):
-        """One decode step for every slot (reference model.py:276-307), enqueued on self.stream."""
-        L = self.lib
-        _lib.check(L.zmi_embed_step(ctypes.byref(self.slots), self.w["emb"].data_ptr(), self.d, self.x.data_ptr(),
-                                    self.row_kv.data_ptr(), self.row_pos.data_ptr(), self.sptr), "embed")
+        """One decode step for every slot (reference model.py:276-307), enqueued on self.stream.
+
+        The step's input embeddings and (kv row, position) tables were written by the previous
+        sampler launch (or the prefill's), fused into its frame-write epilogue."""
         for kind, item in self.plan:
             if kind == "gemv":
                 self._run_gemv(item)
             else:
                 self._attention(item, self.q, self.R, self.row_kv, self.row_pos, self.smax - 1, self.attn)
         self._run_gemv(self._heads)
-        _lib.check(L.zmi_sample_step(ctypes.byref(self.slots), self.logits.data_ptr(),
-                                     None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
-                                     self.samp_cnt.data_ptr(), 0, 0, self.S, self.sptr), "sample")
+        self._sample(self.logits, noise, 0, 0, self.S)
 
     def capture(self):
         if self._graph is None:
@@ -327,9 +339,7 @@ class HipEngine:
                     "step": 0, "total_len": total}
             for k, v in vals.items():
                 st[k][slot] = v
-            _lib.check(L.zmi_sample_step(ctypes.byref(self.slots), self.logits_pre.data_ptr(),
-                                         None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
-                                         self.samp_cnt.data_ptr(), 1, slot, 1, self.sptr), "sample_prefill")
+            self._sample(self.logits_pre, noise, 1, slot, 1)
         return s_len
 
     def _prefill_layers(self, m: int, max_pos: int):
@@ -367,3 +377,4 @@ class HipEngine:
     def release(self, slot: int):
         with torch.cuda.stream(self.stream):
             self.st["active"][slot] = 0
+            self.row_pos[2 * slot: 2 * slot + 2] = -1
