@@ -18,6 +18,7 @@ namespace {
 
 constexpr int CH = 64;
 constexpr int HD = 128;
+constexpr int MAXCH = 16384 / CH;  // RoPE table limit (_torch.py:67) bounds the positions
 
 struct AttnArgs {
   const bf16_t* q;
@@ -167,18 +168,43 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   }
   if (!zmi_last_arriver_wt(a.counters + blockIdx.x, (unsigned)nch, &last_flag)) return;
 
-  float mmax = -INFINITY;
-  for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, ld_wt(base + cc * pstride + g_t * (HD + 2)));
-  float L = 0.f;
+  // merge: all (m, l) of every chunk in one parallel pass, weights in LDS, then an unrolled,
+  // pipelined pass over the chunk outputs (fixed chunk order: deterministic)
+  __shared__ float mw[MAXCH][G], lw[MAXCH][G], Lsum[G];
+  for (int i = t; i < nch * G; i += 256) {
+    const int cc = i / G, g = i - cc * G;
+    mw[cc][g] = ld_wt(base + cc * pstride + g * (HD + 2));
+    lw[cc][g] = ld_wt(base + cc * pstride + g * (HD + 2) + 1);
+  }
+  __syncthreads();
+  if (t < G) {
+    float mmax = -INFINITY;
+    for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, mw[cc][t]);
+    float L = 0.f;
+    for (int cc = 0; cc < nch; ++cc) {
+      const float w = expf(mw[cc][t] - mmax);
+      mw[cc][t] = w;
+      L += w * lw[cc][t];
+    }
+    Lsum[t] = L;
+  }
+  __syncthreads();
   float o[HD / (256 / G) > 0 ? HD / (256 / G) : 1];
   for (int i = 0; i < nd; ++i) o[i] = 0.f;
-  for (int cc = 0; cc < nch; ++cc) {
-    const float* pc = base + cc * pstride + g_t * (HD + 2);
-    const float w = expf(ld_wt(pc) - mmax);
-    L += w * ld_wt(pc + 1);
-    for (int i = 0; i < nd; ++i) o[i] += w * ld_wt(pc + 2 + d_t + i);
+  for (int c0 = 0; c0 < nch; c0 += 8) {
+    float v[8][HD / (256 / G) > 0 ? HD / (256 / G) : 1];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int cc = min(c0 + u, nch - 1);  // clamped loads, zero weight past the end
+      for (int i = 0; i < nd; ++i) v[u][i] = ld_wt(base + cc * pstride + g_t * (HD + 2) + 2 + d_t + i);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float w = (c0 + u < nch) ? mw[c0 + u][g_t] : 0.f;
+      for (int i = 0; i < nd; ++i) o[i] += w * v[u][i];
+    }
   }
-  const float inv_l = 1.0f / L;
+  const float inv_l = 1.0f / Lsum[g_t];
   for (int i = 0; i < nd; ++i)
     a.out[(size_t)qi * a.ldo + (kh * G + g_t) * HD + d_t + i] = (bf16_t)f2bf(o[i] * inv_l);
 }
