@@ -67,6 +67,7 @@ int64_t zmi_gemv_slab_floats(int M, int N, int K, int ksplit); /* ksplit <= 0: l
  * (query row). Replaces F.scaled_dot_product_attention(q, k, v, is_causal, enable_gqa)
  * at zonos/backbone/_torch.py:136 for decode (1 query) and prefill (causal = position bound).
  * ------------------------------------------------------------------------------------- */
+/* q_kv_row may be NULL: query i then reads KV-cache row i (the decode layout). */
 int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                   const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                   int ldo, float* partials, unsigned* counters, void* stream);

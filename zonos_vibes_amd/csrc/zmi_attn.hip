@@ -44,17 +44,15 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   __shared__ unsigned last_flag;
 
   const int qi = blockIdx.x / a.hkv, kh = blockIdx.x - qi * a.hkv, c = blockIdx.y;
-  const int pos = a.pos[qi];
-  if (pos < 0) return;
-  const int nch = pos / CH + 1;
-  if (c >= nch) return;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const size_t kvbase = ((size_t)a.kv_row[qi] * a.hkv + kh) * a.smax * HD;
-  const int plim = min(CH, pos - c * CH + 1);   // valid keys in this chunk
-
-  // ---- issue every load of the block up front (one memory latency) ----
+  // Decode passes kv_row = NULL (row qi caches into KV row qi): the K/V addresses then do not
+  // depend on any load, and the chunk's K/V are requested together with the query position
+  // (rows past the position are loaded but masked; all addresses stay below smax).
+  const int pos = a.pos[qi];
+  const int kvr = a.kv_row ? a.kv_row[qi] : qi;
+  const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
   const int pl = t >> 2, qq = t & 3;                          // scores: key row, quarter of hd
-  const int prow = c * CH + (pl < plim ? pl : plim - 1);      // clamped, no branch around the load
+  const int prow = min(c * CH + pl, a.smax - 1);
   const uint4* kr = reinterpret_cast<const uint4*>(a.k + kvbase + (size_t)prow * HD + qq * 32);
   uint4 kv[4];
 #pragma unroll
@@ -63,15 +61,28 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   uint32_t vv[CH / 4];
 #pragma unroll
   for (int j = 0; j < CH / 4; ++j) {
-    const int p = ph + 4 * j;
-    const int pc = c * CH + (p < plim ? p : plim - 1);
+    const int pc = min(c * CH + ph + 4 * j, a.smax - 1);
     vv[j] = *reinterpret_cast<const uint32_t*>(a.v + kvbase + (size_t)pc * HD + dp);
   }
-  for (int e = t; e < G * HD / 2; e += 256) {
+  uint32_t qv[(G * HD / 2 + 255) / 256];
+#pragma unroll
+  for (int i = 0; i < (G * HD / 2 + 255) / 256; ++i) {
+    const int e = min(t + i * 256, G * HD / 2 - 1);
     const int g = e / (HD / 2), d = (e % (HD / 2)) * 2;
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(a.q + (size_t)qi * a.ldq + (kh * G + g) * HD + d);
-    qs[g][d] = bf2f(v);
-    qs[g][d + 1] = bf2f(v >> 16);
+    qv[i] = *reinterpret_cast<const uint32_t*>(a.q + (size_t)qi * a.ldq + (kh * G + g) * HD + d);
+  }
+  if (pos < 0) return;
+  const int nch = pos / CH + 1;
+  if (c >= nch) return;
+  const int plim = min(CH, pos - c * CH + 1);   // valid keys in this chunk
+#pragma unroll
+  for (int i = 0; i < (G * HD / 2 + 255) / 256; ++i) {
+    const int e = t + i * 256;
+    if (e < G * HD / 2) {
+      const int g = e / (HD / 2), d = (e % (HD / 2)) * 2;
+      qs[g][d] = bf2f(qv[i]);
+      qs[g][d + 1] = bf2f(qv[i] >> 16);
+    }
   }
   __syncthreads();
 
@@ -125,7 +136,8 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < CH / 4; ++j) {
       const int p = ph + 4 * j;
-      const float v0 = bf2f(vv[j]), v1 = bf2f(vv[j] >> 16);
+      const bool ok = p < plim;  // rows past the position were loaded speculatively: never let them in
+      const float v0 = ok ? bf2f(vv[j]) : 0.f, v1 = ok ? bf2f(vv[j] >> 16) : 0.f;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         o0[g] += sc[g][p] * v0;

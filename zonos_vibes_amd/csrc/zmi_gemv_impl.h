@@ -95,12 +95,35 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
       xr[i] = *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + xk0 + c);
     }
   }
+  // epilogue operands needed only at the end, fetched now so their latency hides under the stream
+  // (decode-sized blocks: one (row, column pair) per thread)
+  const int col0 = nt * 16;
+  const bool pre = rows * 16 <= 256;
+  int q_pos = -1, q_kvr = 0;
+  if (EPI == ZMI_EPI_QKV && pre && (int)threadIdx.x < rows * 8) {
+    q_pos = a.row_pos[row0 + (threadIdx.x >> 3)];
+    q_kvr = a.row_kv[row0 + (threadIdx.x >> 3)];
+  }
   __builtin_amdgcn_sched_barrier(0);  // keep the activation loads ahead of the weight stream
   // (2) the weight stream does not depend on the activations: issue chunk 0 right away
   u32x4_t wf[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(wave * NF + f) * 64);
   __builtin_amdgcn_sched_barrier(0);
+  uint32_t res_pre = 0;
+  float2 rope_pre = {1.f, 0.f};
+  if (EPI == ZMI_EPI_RESIDUAL && pre && (int)threadIdx.x < rows * 16) {
+    const int n = col0 + (threadIdx.x & 15);
+    if (n < a.n_valid)
+      res_pre = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + (threadIdx.x >> 4)) * a.ldo + n];
+  }
+  if (EPI == ZMI_EPI_QKV && pre && q_pos >= 0) {
+    const int n = col0 + (threadIdx.x & 7) * 2;
+    if (n < (a.hq + a.hkv) * a.hd) {
+      const int d = (n < a.hq * a.hd ? n : n - a.hq * a.hd) % a.hd;
+      rope_pre = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
+    }
+  }
 
   // (3) activations visible in LDS while the weights are still in flight; LayerNorm statistics
   if (XLDS == XS_DMA) {
@@ -258,7 +281,6 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   }
 
   // ---- fused epilogues ----
-  const int col0 = nt * 16;
   if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32) {
     for (int e = threadIdx.x; e < rows * 16; e += 256) {
       const int m = e >> 4, n = col0 + (e & 15);
@@ -271,7 +293,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
         reinterpret_cast<bf16_t*>(a.out)[o] = (bf16_t)f2bf(v);
       } else {
         bf16_t* p = reinterpret_cast<bf16_t*>(a.out) + o;
-        *p = (bf16_t)f2bf(bf2f(*p) + bfround(v));  // x + bf16(linear(x))  (_torch.py:100-101)
+        const uint32_t xin = pre ? res_pre : (uint32_t)*p;  // prefetched when one element per thread
+        *p = (bf16_t)f2bf(bf2f(xin) + bfround(v));  // x + bf16(linear(x))  (_torch.py:100-101)
       }
     }
   } else if (EPI == ZMI_EPI_LOGITS) {
@@ -297,14 +320,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
     for (int e = threadIdx.x; e < rows * 8; e += 256) {
       const int m = e >> 3, c = (e & 7) * 2;
       const int row = row0 + m;
-      const int pos = a.row_pos[row];
+      const int pos = pre ? q_pos : a.row_pos[row];
       if (pos < 0) continue;
       const int n = col0 + c;
       float x0 = bfround(tile[m][c]), x1 = bfround(tile[m][c + 1]);
       if (n < qcols + kcols) {
         const int d = (n < qcols ? n : n - qcols) % a.hd;
-        const float co = a.rope[((size_t)pos * (a.hd >> 1) + (d >> 1)) * 2];
-        const float si = a.rope[((size_t)pos * (a.hd >> 1) + (d >> 1)) * 2 + 1];
+        const float2 cs =
+            pre ? rope_pre : *reinterpret_cast<const float2*>(a.rope + ((size_t)pos * (a.hd >> 1) + (d >> 1)) * 2);
+        const float co = cs.x, si = cs.y;
         const float r0 = x0 * co - x1 * si;
         const float r1 = x1 * co + x0 * si;
         x0 = r0;
@@ -318,7 +342,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
         const int nn = is_k ? n - qcols : n - qcols - kcols;
         const int kh = nn / a.hd, d = nn - kh * a.hd;
         bf16_t* cache = reinterpret_cast<bf16_t*>(is_k ? a.k_cache : a.v_cache);
-        const size_t o = (((size_t)a.row_kv[row] * a.hkv + kh) * a.smax + pos) * a.hd + d;
+        const size_t o = (((size_t)(pre ? q_kvr : a.row_kv[row]) * a.hkv + kh) * a.smax + pos) * a.hd + d;
         *reinterpret_cast<uint32_t*>(cache + o) = packed;
       }
     }

@@ -160,17 +160,31 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     win_hi = o;
     win_lo = max(0, o - P.rep_window);
   }
+  constexpr int MAXW = 8;  // penalty window tokens held in registers (windows beyond 8 are truncated)
+  int wtok[MAXW];
+  const int nw = min(win_hi - win_lo, MAXW);
+#pragma unroll
+  for (int j = 0; j < MAXW; ++j) wtok[j] = nw > 0 ? min(dl[win_hi - nw + min(j, nw - 1)], NV - 1) : -1;
+  float cv[PER], uv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {  // all logit loads in flight together (clamped index)
+    const int v = min(t + i * 256, NV - 1);
+    cv[i] = lc[v];
+    uv[i] = lu[v];
+  }
+#pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int v = t + i * 256;
     if (v >= NV) break;
-    const float c = lc[v], u = lu[v];
+    const float c = cv[i], u = uv[i];
     float l = u + (c - u) * P.cfg_scale;
     if (v >= 1025) l = -INFINITY;
     if (decode) l = l + ((cb >= 1 && v == ZMI_EOS) ? -INFINITY : 0.0f);
-    if (win_hi > win_lo) {
+    if (nw > 0) {
       float f = 1.0f;
-      for (int j = win_lo; j < win_hi; ++j)
-        if (min(dl[j], NV - 1) == v) f = f * P.rep_penalty;
+#pragma unroll
+      for (int j = 0; j < MAXW; ++j)
+        if (j < nw && wtok[j] == v) f = f * P.rep_penalty;
       l = (l <= 0.f) ? l * f : l / f;
     }
     probs[v] = l;
@@ -299,11 +313,19 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
         nt[idx] = ZMI_EOS;
       }
     }
+    const bool in_range = o < a.sl.total_len[s];
+    const int oc = min(o, a.sl.tcap - 1);
+    int cells[ZMI_NCB];
+#pragma unroll
+    for (int k = 0; k < ZMI_NCB; ++k) cells[k] = a.sl.delayed[((size_t)s * ZMI_NCB + k) * a.sl.tcap + oc];
     int kk = 0;
+#pragma unroll
     for (int k = 0; k < ZMI_NCB; ++k) {
-      int* cell = a.sl.delayed + ((size_t)s * ZMI_NCB + k) * a.sl.tcap + o;
-      int v = o < a.sl.total_len[s] ? *cell : ZMI_MASK;
-      if (o < a.sl.total_len[s] && v == -1) *cell = v = nt[kk++];
+      int v = in_range ? cells[k] : ZMI_MASK;
+      if (in_range && v == -1) {
+        v = nt[kk++];
+        a.sl.delayed[((size_t)s * ZMI_NCB + k) * a.sl.tcap + o] = v;
+      }
       frame[k] = v < 0 ? 0 : (v > ZMI_MASK ? ZMI_MASK : v);  // next step's input frame
     }
     a.sl.offset[s] = o;

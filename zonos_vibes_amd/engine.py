@@ -242,7 +242,7 @@ class HipEngine:
 
     def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
         _lib.check(self.lib.zmi_attention(q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(),
-                                          row_kv.data_ptr(), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
+                                          _lib.ptr(row_kv), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
                                           self.smax, max_pos, out.data_ptr(), self.H * self.hd,
                                           self.attn_part.data_ptr(), self.attn_cnt.data_ptr(), self.sptr), "attention")
 
@@ -269,7 +269,8 @@ class HipEngine:
             if kind == "gemv":
                 self._run_gemv(item)
             else:
-                self._attention(item, self.q, self.R, self.row_kv, self.row_pos, self.smax - 1, self.attn)
+                # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
+                self._attention(item, self.q, self.R, None, self.row_pos, self.smax - 1, self.attn)
         self._run_gemv(self._heads)
         self._sample(self.logits, noise, 0, 0, self.S)
 
