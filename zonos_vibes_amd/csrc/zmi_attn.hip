@@ -104,8 +104,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      dot[g] += __shfl_xor(dot[g], 1, 64);
-      dot[g] += __shfl_xor(dot[g], 2, 64);
+      dot[g] = quad_sum(dot[g]);
     }
     if (qq == 0) {
 #pragma unroll

@@ -39,15 +39,44 @@ __device__ __forceinline__ uint32_t f2h(float f) {
   return (uint32_t)__builtin_bit_cast(uint16_t, v);
 }
 
+// ---- cross-lane reductions on DPP (VALU-speed lane moves, no LDS round trip as ds_bpermute has).
+// All lanes must be active. Each step pairs lanes symmetrically (a+b and b+a), so every lane of a
+// 16-lane row ends with the bit-identical value; the wave total combines the four row values in a
+// fixed order through readlane, so it is uniform too.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141; // lane i <- 7-i within 8
+constexpr int DPP_MIRROR = 0x140;      // lane i <- 15-i within 16
+
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_mov<DPP_XOR1>(v);
+  return v + dpp_mov<DPP_XOR2>(v);
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v = quad_sum(v);
+  v += dpp_mov<DPP_HALF_MIRROR>(v);
+  return v + dpp_mov<DPP_MIRROR>(v);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_mov<DPP_XOR1>(v));
+  v = fmaxf(v, dpp_mov<DPP_XOR2>(v));
+  v = fmaxf(v, dpp_mov<DPP_HALF_MIRROR>(v));
+  return fmaxf(v, dpp_mov<DPP_MIRROR>(v));
+}
+__device__ __forceinline__ float lane_read(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = row16_sum(v);
+  return (lane_read(v, 0) + lane_read(v, 16)) + (lane_read(v, 32) + lane_read(v, 48));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_read(v, 0), lane_read(v, 16)), fmaxf(lane_read(v, 32), lane_read(v, 48)));
 }
 
 // splitmix64 finaliser (shared with zonos_vibes_amd/synthetic.py)
