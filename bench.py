@@ -64,6 +64,16 @@ def time_dominant_kernel(model, reps: int = 3):
     return us, bytes_launch
 
 
+def pmc_traffic():
+    """HBM bytes per fc1 launch from the committed FETCH_SIZE pass (tools/pmc_fc1.py; a counter pass
+    serialises dispatches, so it is not repeated inside the timed run). None if absent."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_fc1.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return int(json.load(f)["hbm_bytes_per_launch"])
+
+
 def time_decode_step(model, steps: int = 64):
     e = model.engine
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -206,10 +216,11 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1),
             "decode_step_hbm_frac": round(step_bytes(model, LC + n_new) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv_kernel<MT=1,NF=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": "gemv_kernel<1,8,LN,SWIGLU,DMA> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": None, "avg_us": round(us, 2),
-                         "bytes_per_launch": bl},
+                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
+                         "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "avg_us": round(us, 2), "bytes_per_launch": bl},
         }
         if world == 1 and not args.no_cpu_baseline:
             sd = {}
