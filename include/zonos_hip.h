@@ -147,6 +147,9 @@ int zmi_graph_end(void* stream, void** graph_exec);
 int zmi_graph_launch(void* graph_exec, int times, void* stream);
 int zmi_graph_destroy(void* graph_exec);
 
+/* Stream [p, p + bytes) through the memory side (Infinity Cache warm-up for a later kernel). */
+int zmi_prefetch(const void* p, int64_t bytes, int blocks, void* stream);
+
 const char* zmi_last_error(void);
 int zmi_version(void);
 

@@ -55,14 +55,10 @@ def gemv(N, K=2048, M=2, ln=True, epi=_lib.EPI_STORE):
     X = torch.randn(M, K, device=dev).to(torch.bfloat16)
     out = torch.zeros(M, N, device=dev).to(torch.bfloat16)
     lw, lb = torch.ones(K, device=dev).to(torch.bfloat16), torch.zeros(K, device=dev).to(torch.bfloat16)
-    ld = L.zmi_row_stats_ld(K)
-    st = torch.ones(M, ld, device=dev)
     a = _lib.GemvArgs()
     a.W, a.X, a.M, a.N, a.K, a.ldx = W.data_ptr(), X.data_ptr(), M, N, K, K
     if ln:
         a.ln_w, a.ln_b, a.eps = lw.data_ptr(), lb.data_ptr(), 1e-5
-    if ln == "stats":
-        a.ln_stats, a.stats_ld = st.data_ptr(), ld
     a.out, a.ldo, a.n_valid = out.data_ptr(), N, N
     s = torch.cuda.current_stream().cuda_stream
     return timed(lambda: _lib.check(L.zmi_gemv_launch(ctypes.byref(a), epi, s)))
@@ -73,5 +69,5 @@ if __name__ == "__main__":
     for R, pos in ((2, 0), (2, 63), (2, 64), (2, 300), (2, 600), (2, 1000), (32, 600)):
         print(json.dumps(dict(probe="attn", R=R, pos=pos, us=round(attn(R, pos), 2))), flush=True)
     for N in (16, 256, 2048, 3072, 16384):
-        for ln in (False, True, "stats"):
+        for ln in (False, True):
             print(json.dumps(dict(probe="gemv_l2_resident", N=N, ln=ln, us=round(gemv(N, ln=ln), 2))), flush=True)

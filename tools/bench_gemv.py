@@ -24,7 +24,7 @@ SHAPES = {  # name: (N, K, epi, ln)
     "fc2": (2048, 8192, _lib.EPI_RESIDUAL, False),
     "heads": (9248, 2048, _lib.EPI_STORE, True),
 }
-VARIANTS = [(1, 0), (1, 2), (1, 4), (2, 0)]  # (ksplit, nchunk; 0 = library choice)
+VARIANTS = [(1, 0), (1, 1), (1, 2), (2, 0), (2, 1), (4, 0), (4, 1), (8, 1), (16, 1)]  # (ksplit, nchunk; 0 = library choice)
 
 
 def timed(fn, reps):

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzonos_hip.so")
+# ZMI_LIB_PATH selects a diagnostic build (tools/stamps.py); the product path is libzonos_hip.so
+LIB_PATH = os.environ.get("ZMI_LIB_PATH") or os.path.join(HERE, "libzonos_hip.so")
 
 c_int, c_int64, c_float, c_void_p, c_uint64 = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, \
     ctypes.c_uint64
@@ -68,6 +69,7 @@ _SIGS = {
                              c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
     "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),
+    "zmi_prefetch": (c_int, [c_void_p, c_int64, c_int, c_void_p]),
     "zmi_graph_begin": (c_int, [c_void_p]),
     "zmi_graph_end": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     "zmi_graph_launch": (c_int, [c_void_p, c_int, c_void_p]),

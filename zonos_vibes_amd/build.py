@@ -10,8 +10,9 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libzonos_hip.so")
+LIB_STAMPS = os.path.join(HERE, "libzonos_hip_stamps.so")
 SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + [ "zmi_attn.hip", "zmi_sample.hip", "zmi_dac.hip", "zmi_misc.hip"]
-HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h"]
+HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_gemv8_impl.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result",
          f"-I{INCLUDE}", f"-I{CSRC}"]
@@ -24,8 +25,11 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
-    objdir = os.path.join(HERE, "build")
+def build(force: bool = False, verbose: bool = True, jobs: int = 8, stamps: bool = False) -> str:
+    """stamps=True builds the diagnostic libzonos_hip_stamps.so (-DZMI_STAMPS, in-kernel timestamps)."""
+    objdir = os.path.join(HERE, "build_stamps" if stamps else "build")
+    lib = LIB_STAMPS if stamps else LIB
+    flags = FLAGS + (["-DZMI_STAMPS"] if stamps else [])
     os.makedirs(objdir, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "zonos_hip.h")]
     objs, procs = [], []
@@ -34,7 +38,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         objs.append(obj)
         if force or _stale(obj, [sp] + hdrs):
-            cmd = [HIPCC, *FLAGS, "-c", sp, "-o", obj]
+            cmd = [HIPCC, *flags, "-c", sp, "-o", obj]
             if verbose:
                 print(" ".join(cmd), flush=True)
             procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -42,12 +46,12 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
                 _wait(procs.pop(0))
     for p in procs:
         _wait(p)
-    if force or _stale(LIB, objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB]
+    if force or _stale(lib, objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", lib]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
-    return LIB
+    return lib
 
 
 def _wait(item):
@@ -61,4 +65,4 @@ def _wait(item):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)

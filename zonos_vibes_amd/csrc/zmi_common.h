@@ -12,6 +12,7 @@
 typedef uint16_t bf16_t;
 typedef uint16_t f16_t;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -20,12 +21,9 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float((h & 0xffffu) << 16); }
 
-__device__ __forceinline__ uint32_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return ((u >> 16) | 0x40u) & 0xffffu;  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
-}
+// fp32 -> bf16 round-to-nearest-even: one v_cvt_pk_bf16_f32 on gfx950 (branch-free; the software
+// form with its NaN test compiles to an exec-mask branch per element)
+__device__ __forceinline__ uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 // round-trip through bf16
 __device__ __forceinline__ float bfround(float f) { return bf2f(f2bf(f)); }

@@ -17,8 +17,10 @@
 //    epilogue: bf16 store, residual add, RoPE + KV-cache write, SwiGLU, or logits.
 //  * Optional LayerNorm prologue (weight+bias, fp32 stats) fuses nn.LayerNorm into the GEMV;
 //    weight loads are issued before the stats so HBM latency hides the reduction.
+#include <cstdlib>
 #include "zmi_common.h"
 #include "zmi_kernels.h"
+#include "zmi_gemv8_impl.h"
 
 namespace zmi_gemv {
 hipError_t launch_epi0(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s);
@@ -27,25 +29,45 @@ hipError_t launch_epi2(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s);
 hipError_t launch_epi3(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s);
 hipError_t launch_epi4(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s);
 hipError_t launch_epi5(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s);
+hipError_t launch8_epi0(const ZmiGemvArgs& a, hipStream_t s);
+hipError_t launch8_epi1(const ZmiGemvArgs& a, hipStream_t s);
+hipError_t launch8_epi2(const ZmiGemvArgs& a, hipStream_t s);
+hipError_t launch8_epi3(const ZmiGemvArgs& a, hipStream_t s);
+hipError_t launch8_epi4(const ZmiGemvArgs& a, hipStream_t s);
+hipError_t launch8_epi5(const ZmiGemvArgs& a, hipStream_t s);
+static hipError_t launch8_epi(const ZmiGemvArgs& a, int epi, hipStream_t s) {
+  switch (epi) {
+    case ZMI_EPI_STORE: return launch8_epi0(a, s);
+    case ZMI_EPI_RESIDUAL: return launch8_epi1(a, s);
+    case ZMI_EPI_QKV: return launch8_epi2(a, s);
+    case ZMI_EPI_SWIGLU: return launch8_epi3(a, s);
+    case ZMI_EPI_LOGITS: return launch8_epi4(a, s);
+    case ZMI_EPI_F32: return launch8_epi5(a, s);
+  }
+  return hipErrorInvalidValue;
+}
 }
 
 namespace {
 
-// Pack a row-major [N_src][K] bf16 weight into MFMA-native tiles (zero rows beyond N_src).
+// Pack a row-major [N_src][K] bf16 weight into the V8 layout (zmi_gemv8_impl.h): 1 KiB chunk
+// (g, kc), lane l = column 8g + (l >> 3), k = 64 kc + 8 (l & 7) .. +7; zero rows beyond N_src.
+// SwiGLU mode interleaves fc1's value and gate halves per group: rows 0..3 of group g are value
+// rows 4g.., rows 4..7 their gates F + 4g.. (F = N_src / 2).
 __global__ void pack_kernel(const bf16_t* __restrict__ src, uint4* __restrict__ dst, int n_src, int k, int n_pad,
                             int mode) {
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const int kt_n = k >> 5;
-  const size_t total = (size_t)(n_pad >> 4) * kt_n * 64;
+  const int kc_n = k >> 6;
+  const size_t total = (size_t)(n_pad >> 3) * kc_n * 64;
   if (idx >= total) return;
   const int l = idx & 63;
   const size_t t = idx >> 6;
-  const int kt = (int)(t % kt_n), nt = (int)(t / kt_n);
-  const int n = nt * 16 + (l & 15), kk = kt * 32 + (l >> 4) * 8;
+  const int kc = (int)(t % kc_n), g = (int)(t / kc_n);
+  const int r = l >> 3, n = g * 8 + r, kk = kc * 64 + (l & 7) * 8;
   int srow = n;
   if (mode == ZMI_PACK_SWIGLU) {
-    const int f = n_src >> 1, c = n & 15;
-    srow = c < 8 ? nt * 8 + c : f + nt * 8 + (c - 8);
+    const int f = n_src >> 1;
+    srow = r < 4 ? g * 4 + r : f + g * 4 + (r - 4);
   }
   uint4 v = {0u, 0u, 0u, 0u};
   if (srow < n_src) v = *reinterpret_cast<const uint4*>(src + (size_t)srow * k + kk);
@@ -80,6 +102,14 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
   ZmiGemvArgs a = *args;
   int mt, nf, ks, nch;
   if (a.N % 16 || a.K % 128) return zmi_fail_msg("gemv: N must be a multiple of 16 and K of 128");
+  if (a.M < 1) return zmi_fail_msg("gemv: M must be >= 1");
+  static const bool mfma_only = getenv("ZMI_GEMV_MFMA") != nullptr;  // A/B switch for measurements
+  if (!mfma_only && a.ksplit <= 1 && zmi_gemv8::use8(a.M, a.N, a.K, a.ln_w != nullptr)) {  // decode regime: 8-column VALU kernel
+    a.nchunk = 1;
+    if (epi < ZMI_EPI_STORE || epi > ZMI_EPI_F32) return zmi_fail_msg("gemv: unknown epilogue");
+    ZMI_CHECK(zmi_gemv::launch8_epi(a, epi, (hipStream_t)stream));
+    return 0;
+  }
   zmi_gemv_plan(a.M, a.N, a.K, &mt, &nf, &ks, &nch);
   if (a.ksplit <= 0) {
     a.ksplit = ks;
@@ -121,9 +151,10 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
 }
 
 extern "C" int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream) {
-  if (n_pad % 16 || k % 32 || n_pad < (mode == ZMI_PACK_SWIGLU ? n_src : 0))
+  if (n_pad % 16 || k % 64 || n_pad < (mode == ZMI_PACK_SWIGLU ? n_src : 0) ||
+      (mode == ZMI_PACK_SWIGLU && (n_src % 8 || n_pad != n_src)))
     return zmi_fail_msg("pack: bad shape");
-  const size_t total = (size_t)(n_pad / 16) * (k / 32) * 64;
+  const size_t total = (size_t)(n_pad / 8) * (k / 64) * 64;
   hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)src, (uint4*)dst, n_src, k, n_pad, mode);
   ZMI_CHECK(hipGetLastError());

@@ -46,7 +46,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X);
   const bf16_t* lnw = reinterpret_cast<const bf16_t*>(a.ln_w);
   const bf16_t* lnb = reinterpret_cast<const bf16_t*>(a.ln_b);
-  const u32x4_t* wbase = reinterpret_cast<const u32x4_t*>(a.W) + ((size_t)nt * KT + kt_base) * 64 + lane;
+  // V8 weight layout (zmi_gemv8_impl.h): the MFMA B fragment (n = lane & 15, k = 8 (lane >> 4) of a
+  // 16 x 32 tile) of K-tile kt sits at  wlane + (kt >> 1) * 64 + (kt & 1) * 4  (uint4 units)
+  const int wn = nt * 16 + (lane & 15);
+  const u32x4_t* wlane = reinterpret_cast<const u32x4_t*>(a.W) + ((size_t)(wn >> 3) * (a.K >> 6)) * 64 +
+                         (wn & 7) * 8 + (lane >> 4);
+  auto wfrag = [&](int kt) { return __builtin_nontemporal_load(wlane + (size_t)(kt >> 1) * 64 + (kt & 1) * 4); };
   const int arow = lane & 15, kq = (lane >> 4) * 8;
 
   // (1) activation rows first (they gate the LayerNorm): up to 4 x 16 B per thread into registers,
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
   // (2) the weight stream does not depend on the activations: issue chunk 0 right away
   u32x4_t wf[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(wave * NF + f) * 64);
+  for (int f = 0; f < NF; ++f) wf[f] = wfrag(kt_base + wave * NF + f);
   __builtin_amdgcn_sched_barrier(0);
   uint32_t res_pre = 0;
   float2 rope_pre = {1.f, 0.f};
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
     const int ktc = (c * 4 + wave) * NF;
     if (c > 0) {
 #pragma unroll
-      for (int f = 0; f < NF; ++f) wf[f] = __builtin_nontemporal_load(wbase + (size_t)(ktc + f) * 64);
+      for (int f = 0; f < NF; ++f) wf[f] = wfrag(kt_base + ktc + f);
     }
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
@@ -306,11 +311,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
       reinterpret_cast<float*>(a.out)[((size_t)(row0 + m) * 9 + cb) * 1026 + v] = bfround(tile[m][e & 15]);
     }
   } else if (EPI == ZMI_EPI_SWIGLU) {
-    // packed tile: columns 0..7 = value rows 8*nt.., 8..15 = gate rows F + 8*nt..  (_torch.py:150-152)
+    // V8 SwiGLU packing: each 8-column group = 4 value rows then their 4 gate rows, so tile
+    // column 8h + c (c < 4) is value row 8nt + 4h + c and 8h + 4 + c its gate  (_torch.py:150-152)
     for (int e = threadIdx.x; e < rows * 8; e += 256) {
-      const int m = e >> 3, c = e & 7;
-      const float y = bfround(tile[m][c]);
-      const float g = bfround(tile[m][c + 8]);
+      const int m = e >> 3, c = e & 7, h = c >> 2, c4 = c & 3;
+      const float y = bfround(tile[m][h * 8 + c4]);
+      const float g = bfround(tile[m][h * 8 + 4 + c4]);
       const float sg = bfround(g / (1.0f + expf(-g)));
       reinterpret_cast<bf16_t*>(a.out)[(size_t)(row0 + m) * a.ldo + nt * 8 + c] = (bf16_t)f2bf(y * sg);
     }

@@ -70,3 +70,35 @@ extern "C" int zmi_graph_destroy(void* graph_exec) {
   if (graph_exec) ZMI_CHECK(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return 0;
 }
+
+// ---- Infinity-Cache (MALL) prefetch: stream a byte range through the memory side so a later
+// kernel's reads of it hit on-die (MI355X_MICROARCH.md "Infinity Cache"). Every lane keeps 8
+// 16-B loads in flight; the loaded values are folded and stored only under a runtime-false flag
+// so the loads cannot be elided.
+namespace {
+__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ p, int64_t n16, unsigned* sink,
+                                                       int never) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  unsigned acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += 8 * stride) {
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t e = i + j * stride;
+      v[j] = p[e < n16 ? e : n16 - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (never) sink[threadIdx.x] = acc;
+}
+}  // namespace
+
+extern "C" int zmi_prefetch(const void* p, int64_t bytes, int blocks, void* stream) {
+  if (bytes < 16) return 0;
+  if (blocks <= 0) blocks = 256;
+  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const uint4*)p, bytes / 16,
+                     (unsigned*)nullptr, 0);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
