@@ -74,6 +74,48 @@ int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cac
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 
 /* ---------------------------------------------------------------------------------------
+ * Persistent decode step: the whole backbone (26 x [LayerNorm -> QKV + RoPE + KV write ->
+ * attention -> out_proj + residual -> LayerNorm -> fc1 + SwiGLU -> fc2 + residual]), norm_f
+ * and the 9 heads in ONE launch of one 1024-thread workgroup per CU. Replaces
+ * TorchZonosBackbone.forward (zonos/backbone/_torch.py:73-152) + _compute_logits
+ * (zonos/model.py:100-116, before CFG) for one decode position of every row.
+ * Each wave runs a static list of weight-slice tasks (host-built, zonos_vibes_amd/step_plan.py)
+ * and issues a task's weights before it waits for the task's input, so the weight stream runs
+ * ahead of the layer's dependency chain; activations move between CUs as 8-byte
+ * {tag, value} granules (MI355X_MICROARCH.md, R2 hand-off). GEMV arithmetic is bit-identical
+ * to zmi_gemv_launch's decode kernel.
+ * ------------------------------------------------------------------------------------- */
+typedef struct ZmiStepLayer {
+  const void *ln1_w, *ln1_b, *ln2_w, *ln2_b; /* bf16 [d]                                       */
+  const void *qkv, *out, *fc1, *fc2;         /* packed weights (zmi_pack_weight; fc1 SWIGLU)     */
+  void *k_cache, *v_cache;                   /* bf16 [rows][hkv][smax][hd] of this layer          */
+} ZmiStepLayer;
+
+typedef struct ZmiStepArgs {
+  const ZmiStepLayer* layers;  /* device [n_layer]                                            */
+  const uint32_t* tasks;       /* device task words (step_plan.py)                            */
+  const int32_t* task_hdr;     /* device [n_blocks][4] = layer_off, layer_len, head_off, head_len */
+  const void* x;               /* bf16 [rows][d] step input (next-step embedding)             */
+  const int* row_pos;          /* [rows] position, < 0 = inactive row                          */
+  const float* rope;           /* [16384][hd/2][2]                                             */
+  const void* heads;           /* packed [9248][d]                                             */
+  const void *nf_w, *nf_b;     /* norm_f                                                       */
+  float* logits;               /* f32 [rows][9][1026]                                          */
+  uint64_t* granules;          /* zmi_step_granule_words(rows, ...) words, zero-initialised    */
+  uint32_t* ctl;               /* 4 words: epoch (init 1), finish ticket, error, spare          */
+  int rows, n_layer, smax, n_blocks, att_cus, att_pmax;
+  float eps;
+} ZmiStepArgs;
+
+/* granule words the step kernel needs for `rows` rows */
+int64_t zmi_step_granule_words(int rows, int n_blocks);
+/* dynamic LDS bytes of one workgroup, or -1 if the configuration does not fit */
+int64_t zmi_step_lds_bytes(int rows, int att_pmax);
+/* CUs of the current device that can each hold one step workgroup (0 = cannot run) */
+int zmi_step_blocks(int rows, int att_pmax);
+int zmi_step_launch(const ZmiStepArgs* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Sampler + EOS state machine + delay-pattern frame write, per utterance slot.
  * Replaces model.py:112-115 (CFG), :266-267/280 (EOS logit bias), sampling.py:99-182
  * (repetition penalty, greedy / softmax / unified / top-p / top-k / min-p / exponential race)

@@ -51,6 +51,25 @@ class Slots(ctypes.Structure):
     ]
 
 
+class StepLayer(ctypes.Structure):
+    _fields_ = [
+        ("ln1_w", c_void_p), ("ln1_b", c_void_p), ("ln2_w", c_void_p), ("ln2_b", c_void_p),
+        ("qkv", c_void_p), ("out", c_void_p), ("fc1", c_void_p), ("fc2", c_void_p),
+        ("k_cache", c_void_p), ("v_cache", c_void_p),
+    ]
+
+
+class StepArgs(ctypes.Structure):
+    _fields_ = [
+        ("layers", c_void_p), ("tasks", c_void_p), ("task_hdr", c_void_p),
+        ("x", c_void_p), ("row_pos", c_void_p), ("rope", c_void_p),
+        ("heads", c_void_p), ("nf_w", c_void_p), ("nf_b", c_void_p), ("logits", c_void_p),
+        ("granules", c_void_p), ("ctl", c_void_p),
+        ("rows", c_int), ("n_layer", c_int), ("smax", c_int), ("n_blocks", c_int),
+        ("att_cus", c_int), ("att_pmax", c_int), ("eps", c_float),
+    ]
+
+
 _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
@@ -58,6 +77,10 @@ _SIGS = {
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "zmi_step_granule_words": (c_int64, [c_int, c_int]),
+    "zmi_step_lds_bytes": (c_int64, [c_int, c_int]),
+    "zmi_step_blocks": (c_int, [c_int, c_int]),
+    "zmi_step_launch": (c_int, [ctypes.POINTER(StepArgs), c_void_p]),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -14,17 +14,21 @@ Batch layout: utterance slot s owns activation / KV rows 2s (conditional) and 2s
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from . import _lib
+from . import step_plan
 from . import synthetic as syn
 from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN, ZonosConfig
 
 HEADS_N = N_CODEBOOKS * 1026            # 9 heads x (1025 + 1 pad row), model.py:37 + utils.py:12-27
 HEADS_N_PAD = (HEADS_N + 15) // 16 * 16
 GEMV_COUNTERS = 1 << 16
+STEP_DIMS = (2048, 16, 4, 128, 8192)   # (d, heads, kv heads, head dim, ffn) the step kernel is built for
 
 
 def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
@@ -71,7 +75,7 @@ def _round8(n: int) -> int:
 
 class HipEngine:
     def __init__(self, cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
-                 max_prefill: int = 512):
+                 max_prefill: int = 512, step_kernel: bool | None = None):
         bb = cfg.backbone
         if bb.ssm_cfg:
             raise NotImplementedError("hybrid (mamba-ssm) backbone is not built (SURVEY.md §8f next #1)")
@@ -94,6 +98,7 @@ class HipEngine:
         self.w = None
         self._graph = None
         self._alloc()
+        self._setup_step(step_kernel)
 
     # ------------------------------------------------------------------ allocation
     def _alloc(self):
@@ -136,6 +141,70 @@ class HipEngine:
                                 self.delayed.data_ptr(), self.params.data_ptr(), self.st["total_len"].data_ptr(),
                                 self.tcap, S)
         self.stream.synchronize()
+
+    def _setup_step(self, want: bool | None):
+        """Persistent decode-step kernel (csrc/zmi_step.hip, plan: step_plan.py) for a one-slot engine
+        at Zonos-v0.1 dims; otherwise (or with ZMI_STEP=0 / step_kernel=False) the per-op launches.
+        want=True makes an unavailable step kernel an error instead of a silent choice."""
+        self.step = None
+        self.step_args = None
+        if want is False or (want is None and os.environ.get("ZMI_STEP", "1") == "0"):
+            return
+        why = None
+        if (self.d, self.H, self.Hkv, self.hd, self.F) != STEP_DIMS:
+            why = f"dims {(self.d, self.H, self.Hkv, self.hd, self.F)} != {STEP_DIMS}"
+        elif self.R != 2:
+            why = f"{self.R} rows (the step kernel runs one CFG slot pair)"
+        else:
+            units = self.R * step_plan.HKV
+            cus = self.lib.zmi_step_blocks(self.R, 1)
+            att = cus // units if cus else 0
+            pmax = -(-self.smax // att) if att else 0
+            if att not in (8, 16, 32, 64) or att * units != cus:
+                why = f"{cus} CUs do not split into {units} attention units of 8/16/32/64"
+            elif self.lib.zmi_step_blocks(self.R, pmax) != cus:
+                why = f"{self.smax} KV positions exceed the step kernel's LDS"
+        if why is not None:
+            if want:
+                raise ValueError(f"step kernel unavailable: {why}")
+            return
+        plan = step_plan.build(cus, self.R)
+        with torch.cuda.stream(self.stream):
+            self.step_tasks = torch.from_numpy(plan.tasks.view(np.int32).copy()).to(self.dev)
+            self.step_hdr = torch.from_numpy(plan.hdr.reshape(-1).copy()).to(self.dev)
+            self.step_gran = torch.zeros(self.lib.zmi_step_granule_words(self.R, cus), dtype=torch.int64,
+                                         device=self.dev)
+            self.step_ctl = torch.tensor([1, 0, 0, 0], dtype=torch.int32).to(self.dev)  # epoch starts at 1
+        self.stream.synchronize()
+        self.step = dict(plan=plan, blocks=cus, att_cus=att, att_pmax=pmax)
+
+    def _build_step_args(self):
+        w = self.w
+        lt = (_lib.StepLayer * self.L)()
+        for i, lw in enumerate(w["layers"]):
+            lt[i] = _lib.StepLayer(lw["ln1_w"].data_ptr(), lw["ln1_b"].data_ptr(), lw["ln2_w"].data_ptr(),
+                                   lw["ln2_b"].data_ptr(), lw["qkv"].data_ptr(), lw["out"].data_ptr(),
+                                   lw["fc1"].data_ptr(), lw["fc2"].data_ptr(), self.kc[i].data_ptr(),
+                                   self.vc[i].data_ptr())
+        with torch.cuda.stream(self.stream):
+            self.step_layers = torch.frombuffer(bytearray(lt), dtype=torch.uint8).to(self.dev)
+        self.stream.synchronize()
+        a = _lib.StepArgs()
+        a.layers, a.tasks, a.task_hdr = self.step_layers.data_ptr(), self.step_tasks.data_ptr(), self.step_hdr.data_ptr()
+        a.x, a.row_pos, a.rope = self.x.data_ptr(), self.row_pos.data_ptr(), self.rope.data_ptr()
+        a.heads, a.nf_w, a.nf_b = w["heads"].data_ptr(), w["nf_w"].data_ptr(), w["nf_b"].data_ptr()
+        a.logits, a.granules, a.ctl = self.logits.data_ptr(), self.step_gran.data_ptr(), self.step_ctl.data_ptr()
+        a.rows, a.n_layer, a.smax = self.R, self.L, self.smax
+        a.n_blocks, a.att_cus, a.att_pmax = self.step["blocks"], self.step["att_cus"], self.step["att_pmax"]
+        a.eps = self.eps
+        self.step_args = a
+
+    def check_step(self):
+        """Raise if the step kernel gave up waiting on a hand-off (its bounded spins set ctl[2])."""
+        if self.step_args is not None:
+            err = int(self.step_ctl[2].item())
+            if err:
+                raise RuntimeError(f"decode-step kernel timed out waiting on a hand-off (code {err:#x})")
 
     def _gemv_shapes(self):
         qkv = (self.H + 2 * self.Hkv) * self.hd
@@ -236,6 +305,8 @@ class HipEngine:
         self._heads = self._gemv(w["heads"], self.x, R, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
                                  n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))
         self.plan = plan
+        if self.step is not None:
+            self._build_step_args()
         if self._graph is not None:
             _lib.check(self.lib.zmi_graph_destroy(self._graph))
             self._graph = None
@@ -265,13 +336,16 @@ class HipEngine:
 
         The step's input embeddings and (kv row, position) tables were written by the previous
         sampler launch (or the prefill's), fused into its frame-write epilogue."""
-        for kind, item in self.plan:
-            if kind == "gemv":
-                self._run_gemv(item)
-            else:
-                # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
-                self._attention(item, self.q, self.R, None, self.row_pos, self.smax - 1, self.attn)
-        self._run_gemv(self._heads)
+        if self.step_args is not None:
+            _lib.check(self.lib.zmi_step_launch(ctypes.byref(self.step_args), self.sptr), "step")
+        else:
+            for kind, item in self.plan:
+                if kind == "gemv":
+                    self._run_gemv(item)
+                else:
+                    # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
+                    self._attention(item, self.q, self.R, None, self.row_pos, self.smax - 1, self.attn)
+            self._run_gemv(self._heads)
         self._sample(self.logits, noise, 0, 0, self.S)
 
     def capture(self):
@@ -359,6 +433,7 @@ class HipEngine:
     # ------------------------------------------------------------------ readback
     def slot_state(self, slot: int) -> dict:
         self.stream.synchronize()
+        self.check_step()
         return {k: int(v[slot].item()) for k, v in self.st.items()}
 
     def read_codes(self, slot: int) -> torch.Tensor:

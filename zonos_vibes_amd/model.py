@@ -29,12 +29,14 @@ def _draw_seed() -> int:
 
 class Zonos:
     def __init__(self, config: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
-                 max_prefill: int = 512, autoencoder: DACAutoencoder | None = None):
+                 max_prefill: int = 512, autoencoder: DACAutoencoder | None = None,
+                 step_kernel: bool | None = None):
         self.config = config
         self.eos_token_id = config.eos_token_id
         self.masked_token_id = config.masked_token_id
         self._device = torch.device(device)
-        self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill)
+        self.step_kernel = step_kernel
+        self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill, step_kernel)
         self.autoencoder = autoencoder if autoencoder is not None else DACAutoencoder(device)
 
     @property
@@ -75,7 +77,7 @@ class Zonos:
         if slots > e.S or seqlen > e.smax or prefill > e.max_prefill:
             w = e.w
             self.engine = HipEngine(self.config, self._device, max(slots, e.S), max(seqlen, e.smax),
-                                    max(prefill, e.max_prefill))
+                                    max(prefill, e.max_prefill), self.step_kernel)
             self.engine.w = w
             self.engine._build_plan()
 
