@@ -103,12 +103,14 @@ typedef struct ZmiStepArgs {
   float* logits;               /* f32 [rows][9][1026]                                          */
   uint64_t* granules;          /* zmi_step_granule_words(rows, ...) words, zero-initialised    */
   uint32_t* ctl;               /* 4 words: epoch (init 1), finish ticket, error, spare          */
+  uint64_t* stamps;            /* NULL; diagnostic build (-DZMI_STAMPS) timestamps               */
   int rows, n_layer, smax, n_blocks, att_cus, att_pmax;
   float eps;
+  int tokens;                  /* weight slices in transit per CU (0 = default 16)              */
 } ZmiStepArgs;
 
 /* granule words the step kernel needs for `rows` rows */
-int64_t zmi_step_granule_words(int rows, int n_blocks);
+int64_t zmi_step_granule_words(int rows, int n_blocks, int n_layer);
 /* dynamic LDS bytes of one workgroup, or -1 if the configuration does not fit */
 int64_t zmi_step_lds_bytes(int rows, int att_pmax);
 /* CUs of the current device that can each hold one step workgroup (0 = cannot run) */

@@ -64,9 +64,9 @@ class StepArgs(ctypes.Structure):
         ("layers", c_void_p), ("tasks", c_void_p), ("task_hdr", c_void_p),
         ("x", c_void_p), ("row_pos", c_void_p), ("rope", c_void_p),
         ("heads", c_void_p), ("nf_w", c_void_p), ("nf_b", c_void_p), ("logits", c_void_p),
-        ("granules", c_void_p), ("ctl", c_void_p),
+        ("granules", c_void_p), ("ctl", c_void_p), ("stamps", c_void_p),
         ("rows", c_int), ("n_layer", c_int), ("smax", c_int), ("n_blocks", c_int),
-        ("att_cus", c_int), ("att_pmax", c_int), ("eps", c_float),
+        ("att_cus", c_int), ("att_pmax", c_int), ("eps", c_float), ("tokens", c_int),
     ]
 
 
@@ -77,7 +77,7 @@ _SIGS = {
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
-    "zmi_step_granule_words": (c_int64, [c_int, c_int]),
+    "zmi_step_granule_words": (c_int64, [c_int, c_int, c_int]),
     "zmi_step_lds_bytes": (c_int64, [c_int, c_int]),
     "zmi_step_blocks": (c_int, [c_int, c_int]),
     "zmi_step_launch": (c_int, [ctypes.POINTER(StepArgs), c_void_p]),

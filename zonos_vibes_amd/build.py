@@ -26,11 +26,13 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8, stamps: bool = False) -> str:
-    """stamps=True builds the diagnostic libzonos_hip_stamps.so (-DZMI_STAMPS, in-kernel timestamps)."""
+def build(force: bool = False, verbose: bool = True, jobs: int = 8, stamps: str | bool = False) -> str:
+    """stamps builds the diagnostic libzonos_hip_stamps.so with in-kernel timestamps: "step" (or True)
+    for the persistent step kernel (-DZMI_STEP_STAMPS, tools/step_stamps.py), "gemv" for the decode
+    GEMV of the launch path (-DZMI_STAMPS, tools/stamps.py; its stamps need a large split-K slab)."""
     objdir = os.path.join(HERE, "build_stamps" if stamps else "build")
     lib = LIB_STAMPS if stamps else LIB
-    flags = FLAGS + (["-DZMI_STAMPS"] if stamps else [])
+    flags = FLAGS + ({"gemv": ["-DZMI_STAMPS"]}.get(stamps, ["-DZMI_STEP_STAMPS"]) if stamps else [])
     os.makedirs(objdir, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "zonos_hip.h")]
     objs, procs = [], []
@@ -66,4 +68,4 @@ def _wait(item):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, stamps="--stamps" in sys.argv)
+    build(force="--force" in sys.argv, stamps="gemv" if "--gemv-stamps" in sys.argv else "--stamps" in sys.argv)

@@ -40,6 +40,8 @@ typedef unsigned long long u64;
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 #define ZLDS __attribute__((address_space(3)))
+#define ZG __attribute__((address_space(1)))  // explicit global space: generic (flat) accesses count
+                                              // in both vmcnt and lgkmcnt and force full drains
 typedef ZLDS bf16_t lbf;  // LDS pointers are declared as such: generic (flat) LDS access is slower
 typedef ZLDS float lfl;
 
@@ -48,15 +50,30 @@ constexpr int D = 2048, F = 8192, HD = 128, HQ = 16, HKV = 4, GQ = HQ / HKV;
 constexpr int QN = HQ * HD, KVN = HKV * HD;  // 2048, 512
 constexpr int NSLOT = 32;
 constexpr int REC = HD + 2;                  // attention partial record per head: m, l, o[128]
+constexpr float ATT_SCALE = 0.08838834764831845f;  // 1 / sqrt(128), SDPA default scale
 constexpr int T_QKV = 0, T_ATT = 1, T_OUT = 2, T_FC1 = 3, T_FC2 = 4, T_HEADS = 5;
 constexpr int FLAGS = 0x00020000;            // buffer descriptor dword3 (as zmi_gemv8)
 constexpr unsigned long long SPIN_LIMIT = 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
 
 struct Gran {  // granule arrays inside the caller's buffer
   gu64 *xg, *qg, *kvg, *ag, *hg, *pg;
+  gu32* hint;  // [layer][nhint] completion counters (hints only: every read is tag-checked)
 };
 
-__device__ __forceinline__ Gran carve(uint64_t* base, int R) {
+// Completion hints. A consumer polls a few 4-byte counters (one lane each) until the producers
+// of an edge have all reported, and only then sweeps the edge's granules (once, usually): the
+// granule tags stay the correctness check, the hints keep waiting waves from re-reading whole
+// edges through the fabric. Shard counters: one per b % 8 (the CUs of one XCD under the observed
+// placement), bumped once per launch by every workgroup of the shard (each owns work of every
+// phase); attention-unit counters: once per launch by each member. Counts accumulate over
+// launches, so the target is epoch x contributors.
+constexpr int H_QKV = 0, H_MERGED = 8, H_OUT = 16, H_FC1 = 24, H_FC2 = 32, H_ATT = 40;
+constexpr int HS = 32;  // u32 stride between counters: each on a 128-B line of its own
+// hint kinds polled per CU (one elected poller each, the other waves wait on the LDS copy)
+constexpr int K_QKV = 0, K_MERGED = 1, K_OUT = 2, K_FC1 = 3, K_FC2 = 4, K_ATT = 5, NKIND = 6;
+__host__ __device__ inline int nhint(int units) { return H_ATT + units; }
+
+__device__ __forceinline__ Gran carve(uint64_t* base, int R, int nb) {
   Gran g;
   gu64* p = ((gu64*)(base));
   g.xg = p;
@@ -65,11 +82,16 @@ __device__ __forceinline__ Gran carve(uint64_t* base, int R) {
   g.ag = g.kvg + R * KVN;
   g.hg = g.ag + R * (QN / 2);
   g.pg = g.hg + R * (F / 2);
+  g.hint = (gu32*)(g.pg + (size_t)nb * GQ * REC);
   return g;
 }
 
 struct Ctl {  // LDS control words
   unsigned cnt[NSLOT];
+  unsigned pdone[8];  // groups of each task type completed on this CU (reset by the last one)
+  int tokens;         // free weight-stream tokens (16 KiB in transit each) of this CU
+  int hseen[8];       // per hint kind: highest layer + 1 this CU has seen complete
+  int hpoll[8];       // per hint kind: 1 while one wave of this CU polls the global counters
   int flag_a, flag_b, att_done, abort_;
 };
 typedef ZLDS Ctl lctl;
@@ -95,21 +117,26 @@ struct Lds {
   lbf* ks;      // [pmax4][HD]
   lbf* vs;      // [pmax4][HD]
   lctl* ctl;
+  const ZLDS struct Args* args;          // the kernel arguments, copied at kernel start
+  const ZLDS ZmiStepLayer* layers;       // the layer table, copied at kernel start
+  const ZLDS int* row_pos;               // [MR]
   int pmax4;
 };
+constexpr int MAXL = 32;  // layer table capacity in LDS
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+struct Args;
+constexpr size_t ARGS_LDS = 256;  // >= sizeof(Args), checked below
 template <int MR>
 __host__ __device__ inline size_t lds_bytes(int pmax4) {
-  size_t b = 0;
+  size_t b = align16(sizeof(Ctl)) + ARGS_LDS + align16(MAXL * sizeof(ZmiStepLayer)) + align16(MR * 4);
   b += 4 * align16((size_t)MR * D * 2);
   b += align16((size_t)NCW * MR * 1024 * 2);
   b += align16((size_t)NSLOT * 64 * MR * 4);
   b += align16((size_t)GQ * HD * 4);
   b += align16((size_t)GQ * pmax4 * 4);
   b += 2 * align16((size_t)pmax4 * HD * 2);
-  b += align16(sizeof(Ctl));
   return b;
 }
 
@@ -122,6 +149,11 @@ __device__ __forceinline__ Lds<MR> carve_lds(ZLDS char* smem, int pmax4) {
     o += align16(bytes);
     return p;
   };
+  // fixed offsets first (readable before pmax4 is known)
+  s.ctl = (lctl*)take(sizeof(Ctl));
+  s.args = (const ZLDS Args*)take(ARGS_LDS);
+  s.layers = (const ZLDS ZmiStepLayer*)take(MAXL * sizeof(ZmiStepLayer));
+  s.row_pos = (const ZLDS int*)take(MR * 4);
   s.xln_a = (lbf*)take((size_t)MR * D * 2);
   s.xln_b = (lbf*)take((size_t)MR * D * 2);
   s.xraw_a = (lbf*)take((size_t)MR * D * 2);
@@ -132,7 +164,6 @@ __device__ __forceinline__ Lds<MR> carve_lds(ZLDS char* smem, int pmax4) {
   s.sc = (lfl*)take((size_t)GQ * pmax4 * 4);
   s.ks = (lbf*)take((size_t)pmax4 * HD * 2);
   s.vs = (lbf*)take((size_t)pmax4 * HD * 2);
-  s.ctl = (lctl*)take(sizeof(Ctl));
   s.pmax4 = pmax4;
   return s;
 }
@@ -149,9 +180,21 @@ struct Args {
   float* logits;
   uint64_t* gran;
   uint32_t* ctl;
-  int L, smax, att_cus, pmax4;
+  unsigned long long* stamps;
+  int L, smax, att_cus, pmax4, tokens;
   float eps, scale;
 };
+static_assert(sizeof(Args) <= ARGS_LDS, "Args must fit its LDS copy");
+
+extern __shared__ __attribute__((aligned(16))) char zsmem[];
+// the view every task function rebuilds from LDS (no pointer to the caller's stack: those are
+// generic and every generic load would drain this wave's outstanding stores)
+template <int MR>
+__device__ __forceinline__ Lds<MR> lds_view() {
+  ZLDS char* base = (ZLDS char*)zsmem;
+  const ZLDS Args* a = (const ZLDS Args*)(base + align16(sizeof(Ctl)));
+  return carve_lds<MR>(base, __builtin_amdgcn_readfirstlane(a->pmax4));
+}
 
 // ---------------------------------------------------------------------------- small helpers
 __device__ __forceinline__ void gran_store(gu64* p, uint32_t tag, uint32_t v) {
@@ -181,13 +224,21 @@ __device__ __forceinline__ float sum8_lanes(float v) {  // as zmi_gemv8::sum8_la
 }
 __device__ __forceinline__ int bcast(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// bounded spin: false (and the CU's abort flag set, the error word tagged) after SPIN_LIMIT
+// Bounded spin: false (and the CU's abort flag set, the error word tagged) after SPIN_LIMIT.
+// A CU runs 4 waves per SIMD and most of them wait most of the time: a short-sleep spin would
+// take the issue slots the computing wave on the same SIMD needs. Waits on LDS state therefore
+// sleep long (SLEEP_LDS x 64 clocks) and whoever changes that state issues s_wakeup, which ends
+// the sleep of every wave of the workgroup; waits on global state (hint counters, granules:
+// nothing on this CU can signal them) poll with a short sleep from one wave per CU.
+constexpr int SLEEP_LDS = 16, SLEEP_GLOBAL = 2;
+__device__ __forceinline__ void wake_all() { asm volatile("s_wakeup" ::: "memory"); }
 struct Spin {
   unsigned long long t0;
   unsigned n;
 };
-__device__ __noinline__ bool spin_on(Spin& sp, lctl* c, uint32_t* ctl, uint32_t code) {
-  __builtin_amdgcn_s_sleep(1);
+template <int SLEEP = SLEEP_GLOBAL>
+__device__ __forceinline__ bool spin_on(Spin& sp, lctl* c, uint32_t* ctl, uint32_t code) {
+  __builtin_amdgcn_s_sleep(SLEEP);
   if ((++sp.n & 31) == 0) {
     if (__hip_atomic_load(&c->abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -207,7 +258,7 @@ __device__ __noinline__ bool spin_on(Spin& sp, lctl* c, uint32_t* ctl, uint32_t 
 __device__ __forceinline__ bool wait_flag(lctl* c, const ZLDS int* flag, int want, uint32_t* ctl, uint32_t code) {
   Spin sp{0, 0};
   while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-    if (!spin_on(sp, c, ctl, code)) return false;
+    if (!spin_on<SLEEP_LDS>(sp, c, ctl, code)) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   return true;
 }
@@ -215,6 +266,116 @@ __device__ __forceinline__ bool wait_flag(lctl* c, const ZLDS int* flag, int wan
 __device__ __forceinline__ uint32_t tag_of(uint32_t epoch, int l, int sub) {
   return (epoch << 6) | ((uint32_t)l << 1) | (uint32_t)sub;
 }
+
+// Wait until counters h[0], h[HS], ... h[(n-1) HS] have all reached `target` (wrap-safe), i.e.
+// layer `want - 1` of hint kind `kind` is complete. One wave per CU polls the global counters
+// (lane i reads counter i); the CU's other waves wait on the LDS copy `hseen[kind]`.
+__device__ __forceinline__ bool wait_hint(lctl* c, int kind, int want, const gu32* h, int n, uint32_t target,
+                                       uint32_t* ctl, uint32_t code, int lane) {
+  Spin sp{0, 0};
+  for (;;) {
+    if (__hip_atomic_load(&c->hseen[kind], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
+    int won = 0;
+    if (lane == 0) {
+      int expect = 0;
+      won = __hip_atomic_compare_exchange_strong(&c->hpoll[kind], &expect, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (bcast(won)) {
+      bool ok = true;
+      for (;;) {
+        if (__hip_atomic_load(&c->hseen[kind], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) break;
+        uint32_t v = target;
+        if (lane < n) v = __hip_atomic_load(h + lane * HS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((int)(v - target) >= 0)) {
+          if (lane == 0) __hip_atomic_fetch_max(&c->hseen[kind], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          wake_all();
+          break;
+        }
+        if (!spin_on(sp, c, ctl, code)) {
+          ok = false;
+          break;
+        }
+      }
+      if (lane == 0) __hip_atomic_store(&c->hpoll[kind], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      wake_all();
+      return ok;
+    }
+    if (!spin_on<SLEEP_LDS>(sp, c, ctl, code)) return false;
+  }
+}
+__device__ __forceinline__ gu32* hint_at(const Gran& g, int units, int l, int k) {
+  return g.hint + ((size_t)l * nhint(units) + k) * HS;
+}
+// one lane bumps a hint counter after this wave's granule stores have been issued (not drained:
+// a hint that overtakes its granules costs the consumer one more sweep, never a wrong value)
+__device__ __forceinline__ void bump(gu32* h, int lane) {
+  if (lane == 0) __hip_atomic_fetch_add(h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Weight-stream tokens. A CU's vector memory path serves its requests in order, so every byte a
+// CU has issued and not yet received sits in front of its next hand-off load. Past ~64 KiB in
+// transit a CU gains no bandwidth (MI355X_MICROARCH.md: ~24 GB/s per CU), only queueing: a
+// wave takes a token before issuing its 16 KiB slice, waits for the slice to land (it has
+// nothing else to do before its input arrives) and returns the token, so at most `tokens`
+// slices are in transit per CU while every wave may hold a landed slice.
+__device__ __forceinline__ bool take_token(lctl* c, uint32_t* ctl, int lane) {
+  Spin sp{0, 0};
+  for (;;) {
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(&c->tokens, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old = bcast(old);
+    if (old > 0) return true;
+    if (lane == 0) __hip_atomic_fetch_add(&c->tokens, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!spin_on<SLEEP_LDS>(sp, c, ctl, 11u)) return false;
+  }
+}
+__device__ __forceinline__ void give_token(lctl* c, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slice has landed
+  if (lane == 0) __hip_atomic_fetch_add(&c->tokens, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  wake_all();
+}
+
+// a group of task type `type` finished on this CU; the CU's last one of the phase bumps the shard
+__device__ __forceinline__ void group_done(lctl* c, int type, int n_on_cu, gu32* shard, int lane) {
+  int old = 0;
+  if (lane == 0)
+    old = (int)__hip_atomic_fetch_add(&c->pdone[type], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = bcast(old);
+  if (old == n_on_cu - 1 && lane == 0) {
+    __hip_atomic_store(&c->pdone[type], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ int groups_on(int total, int b, int nb) { return b < total ? (total - 1 - b) / nb + 1 : 0; }
+__device__ __forceinline__ uint32_t shard_target(uint32_t epoch) { return epoch * (gridDim.x / 8); }
+
+// Diagnostic build only (-DZMI_STEP_STAMPS, tools/step_stamps.py): lane 0 writes s_memrealtime (100 MHz)
+// to stamps[(block, layer, k)]; the product kernel has none.
+#ifdef ZMI_STEP_STAMPS
+#define STEP_STAMP(a, l, k)                                                                         \
+  do {                                                                                              \
+    if ((a).stamps && (threadIdx.x & 63) == 0)                                                      \
+      ((ZG unsigned long long*)(a).stamps)[((size_t)blockIdx.x * ((a).L + 1) + (l)) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// per-task trace of workgroups 0..7: [block][wave][seq][8] after the per-layer stamps
+#define STEP_TRACE(a, seq, k, v)                                                                       \
+  do {                                                                                                \
+    if ((a).stamps && blockIdx.x < 8 && (threadIdx.x & 63) == 0 && (seq) < 128)                        \
+      ((ZG unsigned long long*)(a).stamps)[(size_t)gridDim.x * ((a).L + 1) * 16 +                     \
+                 (((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 128 + (seq)) * 8 + (k)] = (v);      \
+  } while (0)
+#define STEP_TICK(a, seq, k) STEP_TRACE(a, seq, k, __builtin_amdgcn_s_memrealtime())
+#else
+#define STEP_STAMP(a, l, k) \
+  do {                      \
+  } while (0)
+#define STEP_TRACE(a, seq, k, v) \
+  do {                           \
+  } while (0)
+#define STEP_TICK(a, seq, k) \
+  do {                       \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------- stager (wave 15)
 // LayerNorm of MR rows exactly as zmi_gemv8's 256-thread prologue: "thread" c (0..255) owns the
@@ -225,8 +386,10 @@ __device__ __forceinline__ void ln_rows(const lbf* src, const bf16_t* gw, const 
   uint4 gv[4], bv[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
-    gv[w] = *reinterpret_cast<const uint4*>(gw + (lane + 64 * w) * 8);
-    bv[w] = *reinterpret_cast<const uint4*>(gb + (lane + 64 * w) * 8);
+    const u32x4_t g4 = *(const ZG u32x4_t*)(gw + (lane + 64 * w) * 8);
+    const u32x4_t b4 = *(const ZG u32x4_t*)(gb + (lane + 64 * w) * 8);
+    gv[w] = uint4{g4[0], g4[1], g4[2], g4[3]};
+    bv[w] = uint4{b4[0], b4[1], b4[2], b4[3]};
   }
 #pragma unroll 1
   for (int m = 0; m < MR; ++m) {
@@ -310,35 +473,54 @@ __device__ __forceinline__ bool gather_x(lctl* c, const Gran& g, uint32_t tag, l
 // Stage k = 2 l + 1: FC1(l) input (x_mid(l) granules) -> x_mid raw + LN2 rows, flag_b = l + 1.
 // Stage k = 2 L: x_out(L-1) -> norm_f rows, flag_b = L + 1. One call site per helper (code size).
 template <int MR>
-__device__ __noinline__ void stager(const Args& a, const Lds<MR>& s, const Gran& g, uint32_t epoch, int lane) {
+__device__ __forceinline__ void stager(uint32_t epoch, int lane) {
+  const Lds<MR> s = lds_view<MR>();
+  const ZLDS Args& a = *s.args;
+  const Gran g = carve((uint64_t*)uni(a.gran), MR, gridDim.x);
+  epoch = __builtin_amdgcn_readfirstlane(epoch);
 #pragma unroll 1
   for (int k = 0; k <= 2 * a.L; ++k) {
     const int l = k >> 1;
     const bool second = (k & 1) != 0, last = k == 2 * a.L;
     // raw rows: x_in (out_proj residual), x_mid (fc2 residual); norm_f normalises in place
     lbf* raw = last ? s.xln_b : (second ? s.xraw_b : s.xraw_a);
+    STEP_TICK(a, k, 0);
+    STEP_TRACE(a, k, 6, (unsigned long long)l);
+    STEP_TRACE(a, k, 7, (unsigned long long)(7 | (k << 8)));
     if (k == 0) {
 #pragma unroll
       for (int m = 0; m < MR; ++m)
 #pragma unroll
         for (int w = 0; w < 4; ++w)
-          lds16(raw + m * D + (lane + 64 * w) * 8, *reinterpret_cast<const uint4*>(a.x + m * D + (lane + 64 * w) * 8));
+        {
+          const u32x4_t v = *(const ZG u32x4_t*)(a.x + m * D + (lane + 64 * w) * 8);
+          lds16(raw + m * D + (lane + 64 * w) * 8, uint4{v[0], v[1], v[2], v[3]});
+        }
     } else {
       const uint32_t tag = second ? tag_of(epoch, l, 0) : tag_of(epoch, l - 1, 1);
+      const gu32* h = hint_at(g, MR * HKV, second ? l : l - 1, second ? H_OUT : H_FC2);
+      if (!wait_hint(s.ctl, second ? K_OUT : K_FC2, second ? l + 1 : l, h, 8, shard_target(epoch), a.ctl, 7u, lane))
+        return;
+      STEP_TICK(a, k, 1);
       if (!gather_x<MR>(s.ctl, g, tag, raw, a.ctl, lane)) return;
     }
+    STEP_TICK(a, k, 2);
+    STEP_STAMP(a, l, second ? 2 : 0);
     const bf16_t *gw, *gb;
     if (last) {
       gw = a.nf_w;
       gb = a.nf_b;
     } else {
-      const ZmiStepLayer& ly = a.layers[l];
+      const ZLDS ZmiStepLayer& ly = s.layers[l];
       gw = (const bf16_t*)(second ? ly.ln2_w : ly.ln1_w);
       gb = (const bf16_t*)(second ? ly.ln2_b : ly.ln1_b);
     }
     ln_rows<MR>(raw, gw, gb, a.eps, second || last ? s.xln_b : s.xln_a, lane);
     __hip_atomic_store(second || last ? &s.ctl->flag_b : &s.ctl->flag_a, l + 1, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
+    wake_all();
+    STEP_STAMP(a, l, second ? 3 : 1);
+    STEP_TICK(a, k, 4);
   }
 }
 
@@ -384,11 +566,21 @@ __device__ __forceinline__ bool sweep_slice(lctl* c, const gu64* src, int row_wo
 }
 
 template <int MR, int KIND>
-__device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gran& gr, uint32_t epoch, int l, int g, int wk,
-                          int slot, int wave, int lane) {
+__device__ __forceinline__ bool gemv_task(uint32_t epoch, int l, int g, int wk, int slot, int wave, int lane, int seq) {
+  const Lds<MR> s = lds_view<MR>();
+  const ZLDS Args& a = *s.args;
+  const Gran gr = carve((uint64_t*)uni(a.gran), MR, gridDim.x);
+  epoch = __builtin_amdgcn_readfirstlane(epoch);
+  l = __builtin_amdgcn_readfirstlane(l);
+  g = __builtin_amdgcn_readfirstlane(g);
+  wk = __builtin_amdgcn_readfirstlane(wk);
+  slot = __builtin_amdgcn_readfirstlane(slot);
+  wave = __builtin_amdgcn_readfirstlane(wave);
+  seq = __builtin_amdgcn_readfirstlane(seq);
+  STEP_TICK(a, seq, 0);
   using P = Phase<KIND>;
   constexpr int W = P::W, NL = P::NL, K = P::K, KC = K / 64;
-  const ZmiStepLayer* ly = a.layers + (KIND == T_HEADS ? 0 : l);
+  const ZLDS ZmiStepLayer* ly = s.layers + (KIND == T_HEADS ? 0 : l);
   const char* wp = KIND == T_QKV   ? (const char*)ly->qkv
                    : KIND == T_OUT ? (const char*)ly->out
                    : KIND == T_FC1 ? (const char*)ly->fc1
@@ -400,19 +592,24 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
   int q_pos = -1;
   float2 cs = {1.f, 0.f};
   if (KIND == T_QKV && et < 4 * MR) {
-    q_pos = a.row_pos[et >> 2];
+    q_pos = s.row_pos[et >> 2];
     const int n = col0 + (et & 3) * 2;
     if (n < QN + KVN && q_pos >= 0) {
       const int d = (n < QN ? n : n - QN) % HD;
-      cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (HD / 2) + (d >> 1)) * 2);
+      const ZG float* rp = (const ZG float*)a.rope + ((size_t)q_pos * (HD / 2) + (d >> 1)) * 2;
+      cs = float2{rp[0], rp[1]};
     }
   }
   __builtin_amdgcn_sched_barrier(0);
+  if (!take_token(s.ctl, a.ctl, lane)) return false;
   const __amdgpu_buffer_rsrc_t wr = rsrc_of(wp + ((size_t)g * KC + wk * NL) * 1024, NL * 1024);
   u32x4_t wf[NL];
 #pragma unroll
   for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 16, j * 1024, 2 /* nt */);
   __builtin_amdgcn_sched_barrier(0);
+  give_token(s.ctl, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  STEP_TICK(a, seq, 1);
 
   // input rows of this task's k-range
   const lbf* xrow[MR];
@@ -426,11 +623,19 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
     lbf* dst = s.win + wave * MR * 1024;
     const gu64* src = KIND == T_OUT ? gr.ag : gr.hg;
     const int row_words = KIND == T_OUT ? QN / 2 : F / 2;
+    const gu32* h = hint_at(gr, MR * HKV, l, KIND == T_OUT ? H_MERGED : H_FC1);
+    if (!wait_hint(s.ctl, KIND == T_OUT ? K_MERGED : K_FC1, l + 1, h, 8, shard_target(epoch), a.ctl, 8u, lane))
+      return false;
     if (!sweep_slice<MR, NL>(s.ctl, src, row_words, wk * NL * 32, tag_of(epoch, l, 0), dst, a.ctl, lane))
       return false;
 #pragma unroll
     for (int m = 0; m < MR; ++m) xrow[m] = dst + m * (NL * 64) + (lane & 7) * 8;
   }
+  STEP_TICK(a, seq, 2);
+  if (KIND == T_OUT) STEP_STAMP(a, l, 7);
+  if (KIND == T_FC1) STEP_STAMP(a, l, 8);
+  if (KIND == T_FC2) STEP_STAMP(a, l, 9);
+  if (KIND == T_QKV) STEP_STAMP(a, l, 11);
 
   // dot products (zmi_gemv8 step 4, verbatim order)
   float acc[MR];
@@ -465,6 +670,9 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
   if (lane == 0)
     old = (int)__hip_atomic_fetch_add(&s.ctl->cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
   old = bcast(old);
+  STEP_TICK(a, seq, 3);
+  STEP_TRACE(a, seq, 6, (unsigned long long)l);
+  STEP_TRACE(a, seq, 7, (unsigned long long)(KIND | (g << 8) | (old << 24)));
   if (old != W - 1) return true;
   if (lane == 0) __hip_atomic_store(&s.ctl->cnt[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   auto colsum = [&](int c, int m) {
@@ -495,8 +703,8 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
         if (q_pos >= 0) {  // KV cache write at this position (_torch.py:33-49)
           const bool is_k = nn < KVN;
           const int kk = is_k ? nn : nn - KVN, kh = kk / HD, d = kk - kh * HD;
-          bf16_t* cache = reinterpret_cast<bf16_t*>(is_k ? ly->k_cache : ly->v_cache);
-          *reinterpret_cast<uint32_t*>(cache + (((size_t)m * HKV + kh) * a.smax + q_pos) * HD + d) = packed;
+          ZG bf16_t* cache = (ZG bf16_t*)(is_k ? ly->k_cache : ly->v_cache);
+          *(ZG uint32_t*)(cache + (((size_t)m * HKV + kh) * a.smax + q_pos) * HD + d) = packed;
         }
       }
     }
@@ -527,10 +735,21 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
       const int m = et >> 3, c = et & 7, n = col0 + c;
       if (n < ZMI_NCB * ZMI_VOCAB) {
         const int cb = n / ZMI_VOCAB, vv = n - cb * ZMI_VOCAB;
-        a.logits[((size_t)m * ZMI_NCB + cb) * ZMI_VOCAB + vv] = bfround(colsum(c, m));
+        ((ZG float*)a.logits)[((size_t)m * ZMI_NCB + cb) * ZMI_VOCAB + vv] = bfround(colsum(c, m));
       }
     }
   }
+  if (KIND != T_HEADS) {
+    constexpr int H = KIND == T_QKV ? H_QKV : (KIND == T_OUT ? H_OUT : (KIND == T_FC1 ? H_FC1 : H_FC2));
+    constexpr int G = KIND == T_QKV ? (QN + 2 * KVN) / 8 : (KIND == T_FC1 ? 2 * F / 8 : D / 8);
+    group_done(s.ctl, KIND, groups_on(G, blockIdx.x, gridDim.x), hint_at(gr, MR * HKV, l, H + (blockIdx.x & 7)),
+               lane);
+  }
+  STEP_TICK(a, seq, 4);
+  if (KIND == T_FC2) STEP_STAMP(a, l, 10);
+  if (KIND == T_QKV) STEP_STAMP(a, l, 12);
+  if (KIND == T_FC1) STEP_STAMP(a, l, 13);
+  if (KIND == T_OUT) STEP_STAMP(a, l, 14);
   return true;
 }
 
@@ -540,19 +759,30 @@ __device__ __noinline__ bool gemv_task(const Args& a, const Lds<MR>& s, const Gr
 // SDPA scale 1/sqrt(128)). Partials (m, l, o) are published as granules; then every member merges
 // its 512 / att_cus dims of the 4 heads over all members (fixed lane-tree order: deterministic).
 template <int MR>
-__device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gran& gr, uint32_t epoch, int l, int u, int j,
-                         int lane) {
+__device__ __forceinline__ bool att_task(uint32_t epoch, int l, int u, int j, int lane, int seq) {
+  const Lds<MR> s = lds_view<MR>();
+  const ZLDS Args& a = *s.args;
+  const Gran gr = carve((uint64_t*)uni(a.gran), MR, gridDim.x);
+  epoch = __builtin_amdgcn_readfirstlane(epoch);
+  l = __builtin_amdgcn_readfirstlane(l);
+  u = __builtin_amdgcn_readfirstlane(u);
+  j = __builtin_amdgcn_readfirstlane(j);
+  seq = __builtin_amdgcn_readfirstlane(seq);
+  STEP_TICK(a, seq, 0);
+  STEP_TRACE(a, seq, 6, (unsigned long long)l);
+  STEP_TRACE(a, seq, 7, (unsigned long long)(T_ATT | (u << 8)));
   const int r = u / HKV, kvh = u - r * HKV, ncu = a.att_cus;
   // the previous layer's attention on this CU must be done with the LDS scratch
   if (!wait_flag(s.ctl, &s.ctl->att_done, l, a.ctl, 4u)) return false;
-  const int pos = a.row_pos[r];
-  const ZmiStepLayer& ly = a.layers[l];
+  const int pos = __builtin_amdgcn_readfirstlane(s.row_pos[r]);
+  const ZLDS ZmiStepLayer& ly = s.layers[l];
   const uint32_t tag = tag_of(epoch, l, 0);
   const int np = (pos >= j) ? (pos - j) / ncu + 1 : 0;  // my positions, the last may be `pos`
   const bool own_new = np > 0 && (j + (np - 1) * ncu == pos);
   const int nhist = own_new ? np - 1 : np;
   const size_t kvbase = ((size_t)r * HKV + kvh) * a.smax * HD;
   // (1) history K/V rows -> LDS by DMA, 4 rows (1 KiB) per instruction
+  if (!take_token(s.ctl, a.ctl, lane)) return false;
   {
     const int pl = lane >> 4;  // row within the 4-row piece
     for (int t = 0; t < (nhist + 3) / 4; ++t) {
@@ -573,15 +803,21 @@ __device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gra
       }
     }
   }
+  give_token(s.ctl, lane);
+  STEP_TICK(a, seq, 1);
   if (pos < 0) {  // inactive row: zero output slice, nothing else to hand off
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int dpc = (GQ * HD) / ncu;
     const int h = (j * dpc) / HD, d0 = (j * dpc) % HD;
     if (lane < dpc / 2) gran_store(gr.ag + r * (QN / 2) + ((kvh * GQ + h) * HD + d0) / 2 + lane, tag, 0u);
     if (lane == 0) __hip_atomic_store(&s.ctl->att_done, l + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wake_all();
+    bump(hint_at(gr, MR * HKV, l, H_ATT + u), lane);  // counts accumulate over launches: every path adds
+    bump(hint_at(gr, MR * HKV, l, H_MERGED + (blockIdx.x & 7)), lane);
     return true;
   }
   // (2) q of the 4 heads (+ the new k/v row when this CU owns `pos`), granules
+  if (!wait_hint(s.ctl, K_QKV, l + 1, hint_at(gr, MR * HKV, l, H_QKV), 8, shard_target(epoch), a.ctl, 9u, lane))
+    return false;
   {
     const __amdgpu_buffer_rsrc_t rq = rsrc_of(gr.qg + r * (QN / 2) + kvh * GQ * (HD / 2), GQ * (HD / 2) * 8);
     const __amdgpu_buffer_rsrc_t rk = rsrc_of(gr.kvg + r * KVN + kvh * (HD / 2), (HD / 2) * 8);
@@ -616,6 +852,8 @@ __device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gra
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  STEP_STAMP(a, l, 4);
+  STEP_TICK(a, seq, 2);
   // (3) scores: 4 lanes per key row (32 dims each), 16 rows per pass
   const int pm = s.pmax4;
   {
@@ -640,7 +878,7 @@ __device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gra
 #pragma unroll
       for (int h = 0; h < GQ; ++h) {
         const float v = quad_sum(dot[h]);
-        if (qq == 0 && i < np) s.sc[h * pm + i] = v * a.scale;
+        if (qq == 0 && i < np) s.sc[h * pm + i] = v * ATT_SCALE;
       }
     }
   }
@@ -691,25 +929,33 @@ __device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gra
     gran_store(rec + lane * REC, tag, __float_as_uint(m));
     gran_store(rec + lane * REC + 1, tag, __float_as_uint(lsum));
   }
+  STEP_TICK(a, seq, 3);
+  bump(hint_at(gr, MR * HKV, l, H_ATT + u), lane);
   // the LDS scratch is free again
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  STEP_STAMP(a, l, 5);
   if (lane == 0) __hip_atomic_store(&s.ctl->att_done, l + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  wake_all();
 
   // (7) merge my slice: dims [d0, d0 + dpc) of head hm, over all members jj (lpp lanes each,
   // 8 dims per lane)
   const int dpc = (GQ * HD) / ncu, lpp = 64 / ncu;
   const int hm = (j * dpc) / HD, d0 = (j * dpc) % HD;
   const int jj = lane / lpp, sub = lane - jj * lpp;
-  const gu64* mrec = gr.pg + ((size_t)u * ncu + jj) * GQ * REC + hm * REC;
-  const __amdgpu_buffer_rsrc_t rm = rsrc_of(mrec, REC * 8);
+  // descriptor on the unit's (uniform) record base; the member index goes into the lane offset
+  const __amdgpu_buffer_rsrc_t rm = rsrc_of(gr.pg + (size_t)u * ncu * GQ * REC, ncu * GQ * REC * 8);
+  const int mo = (jj * GQ * REC + hm * REC) * 8;
   float mv = 0.f, lv = 0.f, ov[8];
+  if (!wait_hint(s.ctl, K_ATT, l + 1, hint_at(gr, MR * HKV, l, H_ATT + u), 1, epoch * (uint32_t)ncu, a.ctl, 10u,
+                 lane))
+    return false;
   {
     Spin sp{0, 0};
     for (;;) {
-      const u32x4_t ml = ld_sc1(rm, 0);
+      const u32x4_t ml = ld_sc1(rm, mo);
       u32x4_t ob[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) ob[t] = ld_sc1(rm, (2 + d0 + sub * 8 + 2 * t) * 8);
+      for (int t = 0; t < 4; ++t) ob[t] = ld_sc1(rm, mo + (2 + d0 + sub * 8 + 2 * t) * 8);
       bool ok = (ml[1] == tag) & (ml[3] == tag);
 #pragma unroll
       for (int t = 0; t < 4; ++t) ok &= (ob[t][1] == tag) & (ob[t][3] == tag);
@@ -743,30 +989,44 @@ __device__ __noinline__ bool att_task(const Args& a, const Lds<MR>& s, const Gra
 #pragma unroll
     for (int e = 0; e < 4; ++e) gran_store(dst + e, tag, f2bf(ov[2 * e] * inv) | (f2bf(ov[2 * e + 1] * inv) << 16));
   }
+  STEP_TICK(a, seq, 5);
+  bump(hint_at(gr, MR * HKV, l, H_MERGED + (blockIdx.x & 7)), lane);
+  STEP_STAMP(a, l, 6);
+  STEP_TICK(a, seq, 4);
   return true;
 }
 
 // ---------------------------------------------------------------------------- the kernel
 template <int MR>
 __global__ __launch_bounds__(NT, 4) void step_kernel(const Args a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds<MR> s = carve_lds<MR>((ZLDS char*)smem, a.pmax4);
+  const Lds<MR> s = carve_lds<MR>((ZLDS char*)zsmem, a.pmax4);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < NSLOT) s.ctl->cnt[tid] = 0;
+  if (tid < 8) {
+    s.ctl->pdone[tid] = 0;
+    s.ctl->hseen[tid] = 0;
+    s.ctl->hpoll[tid] = 0;
+  }
   if (tid == 0) {
     s.ctl->flag_a = 0;
     s.ctl->flag_b = 0;
     s.ctl->att_done = 0;
     s.ctl->abort_ = 0;
+    s.ctl->tokens = a.tokens;
   }
+  // kernel arguments, layer table and row positions into LDS (task functions read them there)
+  if (tid < (int)(sizeof(Args) / 4)) ((ZLDS uint32_t*)s.args)[tid] = reinterpret_cast<const uint32_t*>(&a)[tid];
+  for (int i = tid; i < a.L * (int)(sizeof(ZmiStepLayer) / 8); i += NT)
+    ((ZLDS uint64_t*)s.layers)[i] = ((const ZG uint64_t*)a.layers)[i];
+  if (tid < MR) ((ZLDS int*)s.row_pos)[tid] = ((const ZG int*)a.row_pos)[tid];
   __syncthreads();
   const uint32_t epoch = __builtin_amdgcn_readfirstlane(
       __hip_atomic_load(((gu32*)(a.ctl)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const Gran g = carve(a.gran, MR);
+  const Gran g = carve((uint64_t*)uni(a.gran), MR, gridDim.x);
 
   if (wave == NWAVES - 1) {
-    stager<MR>(a, s, g, epoch, lane);
+    stager<MR>(epoch, lane);
   } else {
     const int4 h = a.hdr[blockIdx.x];
     const int nlayer = a.L * h.y, total = nlayer + h.w;
@@ -783,13 +1043,14 @@ __global__ __launch_bounds__(NT, 4) void step_kernel(const Args a) {
       t = __builtin_amdgcn_readfirstlane(t);
       const int type = t & 7, wk = (t >> 3) & 15, grp = (t >> 7) & 8191, slot = (t >> 20) & 255;
       bool ok = true;
+      const int seq = i / NCW;
       switch (type) {
-        case T_QKV: ok = gemv_task<MR, T_QKV>(a, s, g, epoch, l, grp, wk, slot, wave, lane); break;
-        case T_ATT: ok = att_task<MR>(a, s, g, epoch, l, grp, slot, lane); break;
-        case T_OUT: ok = gemv_task<MR, T_OUT>(a, s, g, epoch, l, grp, wk, slot, wave, lane); break;
-        case T_FC1: ok = gemv_task<MR, T_FC1>(a, s, g, epoch, l, grp, wk, slot, wave, lane); break;
-        case T_FC2: ok = gemv_task<MR, T_FC2>(a, s, g, epoch, l, grp, wk, slot, wave, lane); break;
-        default: ok = gemv_task<MR, T_HEADS>(a, s, g, epoch, a.L, grp, wk, slot, wave, lane); break;
+        case T_QKV: ok = gemv_task<MR, T_QKV>(epoch, l, grp, wk, slot, wave, lane, seq); break;
+        case T_ATT: ok = att_task<MR>(epoch, l, grp, slot, lane, seq); break;
+        case T_OUT: ok = gemv_task<MR, T_OUT>(epoch, l, grp, wk, slot, wave, lane, seq); break;
+        case T_FC1: ok = gemv_task<MR, T_FC1>(epoch, l, grp, wk, slot, wave, lane, seq); break;
+        case T_FC2: ok = gemv_task<MR, T_FC2>(epoch, l, grp, wk, slot, wave, lane, seq); break;
+        default: ok = gemv_task<MR, T_HEADS>(epoch, a.L, grp, wk, slot, wave, lane, seq); break;
       }
       if (!ok) break;
     }
@@ -821,10 +1082,12 @@ int launch(const ZmiStepArgs* z, hipStream_t stream) {
   a.logits = z->logits;
   a.gran = z->granules;
   a.ctl = z->ctl;
+  a.stamps = (unsigned long long*)z->stamps;
   a.L = z->n_layer;
   a.smax = z->smax;
   a.att_cus = z->att_cus;
   a.pmax4 = (z->att_pmax + 3) & ~3;
+  a.tokens = z->tokens > 0 ? z->tokens : 16;
   a.eps = z->eps;
   a.scale = 1.0f / sqrtf((float)HD);
   const size_t lds = lds_bytes<MR>(a.pmax4);
@@ -840,8 +1103,9 @@ int launch(const ZmiStepArgs* z, hipStream_t stream) {
 
 using namespace zmi_step;
 
-extern "C" int64_t zmi_step_granule_words(int rows, int n_blocks) {
-  return (int64_t)rows * (D / 2 + QN / 2 + KVN + QN / 2 + F / 2) + (int64_t)n_blocks * GQ * REC;
+extern "C" int64_t zmi_step_granule_words(int rows, int n_blocks, int n_layer) {
+  return (int64_t)rows * (D / 2 + QN / 2 + KVN + QN / 2 + F / 2) + (int64_t)n_blocks * GQ * REC +
+         (int64_t)n_layer * nhint(rows * HKV) * HS / 2;
 }
 
 extern "C" int64_t zmi_step_lds_bytes(int rows, int att_pmax) {
@@ -869,9 +1133,11 @@ extern "C" int zmi_step_blocks(int rows, int att_pmax) {
 extern "C" int zmi_step_launch(const ZmiStepArgs* z, void* stream) {
   if (!z || !z->layers || !z->tasks || !z->task_hdr || !z->granules || !z->ctl)
     return zmi_fail_msg("step: null argument");
+  if (z->n_blocks % 8) return zmi_fail_msg("step: n_blocks must be a multiple of 8 (hint shards)");
   if (z->n_blocks <= 0 || z->att_cus < 8 || 64 % z->att_cus != 0 || z->rows * HKV * z->att_cus != z->n_blocks)
     return zmi_fail_msg("step: n_blocks must equal rows * 4 * att_cus with att_cus in {8, 16, 32, 64}");
   if ((int64_t)z->att_pmax * z->att_cus < z->smax) return zmi_fail_msg("step: att_pmax * att_cus < smax");
+  if (z->n_layer < 1 || z->n_layer > MAXL) return zmi_fail_msg("step: n_layer must be in [1, 32]");
   if (zmi_step_lds_bytes(z->rows, z->att_pmax) < 0) return zmi_fail_msg("step: configuration exceeds LDS");
   switch (z->rows) {
     case 2: return launch<2>(z, (hipStream_t)stream);

@@ -144,11 +144,14 @@ class HipEngine:
 
     def _setup_step(self, want: bool | None):
         """Persistent decode-step kernel (csrc/zmi_step.hip, plan: step_plan.py) for a one-slot engine
-        at Zonos-v0.1 dims; otherwise (or with ZMI_STEP=0 / step_kernel=False) the per-op launches.
+        at Zonos-v0.1 dims, when asked for (step_kernel=True or ZMI_STEP=1); otherwise the per-op
+        launches captured in a hipGraph. The launch path is the default: measured at C2 (p = 591) it
+        takes 1.15 ms per step against 1.87 ms for the step kernel, whose grid-wide hand-offs cost
+        more than the launch boundaries they remove.
         want=True makes an unavailable step kernel an error instead of a silent choice."""
-        self.step = None
+        self.step_cfg = None
         self.step_args = None
-        if want is False or (want is None and os.environ.get("ZMI_STEP", "1") == "0"):
+        if want is False or (want is None and os.environ.get("ZMI_STEP", "0") != "1"):
             return
         why = None
         if (self.d, self.H, self.Hkv, self.hd, self.F) != STEP_DIMS:
@@ -172,11 +175,11 @@ class HipEngine:
         with torch.cuda.stream(self.stream):
             self.step_tasks = torch.from_numpy(plan.tasks.view(np.int32).copy()).to(self.dev)
             self.step_hdr = torch.from_numpy(plan.hdr.reshape(-1).copy()).to(self.dev)
-            self.step_gran = torch.zeros(self.lib.zmi_step_granule_words(self.R, cus), dtype=torch.int64,
+            self.step_gran = torch.zeros(self.lib.zmi_step_granule_words(self.R, cus, self.L), dtype=torch.int64,
                                          device=self.dev)
             self.step_ctl = torch.tensor([1, 0, 0, 0], dtype=torch.int32).to(self.dev)  # epoch starts at 1
         self.stream.synchronize()
-        self.step = dict(plan=plan, blocks=cus, att_cus=att, att_pmax=pmax)
+        self.step_cfg = dict(plan=plan, blocks=cus, att_cus=att, att_pmax=pmax)
 
     def _build_step_args(self):
         w = self.w
@@ -195,8 +198,13 @@ class HipEngine:
         a.heads, a.nf_w, a.nf_b = w["heads"].data_ptr(), w["nf_w"].data_ptr(), w["nf_b"].data_ptr()
         a.logits, a.granules, a.ctl = self.logits.data_ptr(), self.step_gran.data_ptr(), self.step_ctl.data_ptr()
         a.rows, a.n_layer, a.smax = self.R, self.L, self.smax
-        a.n_blocks, a.att_cus, a.att_pmax = self.step["blocks"], self.step["att_cus"], self.step["att_pmax"]
+        a.n_blocks, a.att_cus, a.att_pmax = self.step_cfg["blocks"], self.step_cfg["att_cus"], self.step_cfg["att_pmax"]
         a.eps = self.eps
+        a.tokens = int(os.environ.get("ZMI_STEP_TOKENS", "0"))  # tuning knob; 0 = library default
+        if os.environ.get("ZMI_STEP_STAMPS"):  # diagnostic build only (tools/step_stamps.py)
+            self.step_stamps = torch.zeros(self.step_cfg["blocks"] * (self.L + 1) * 16 + 8 * 16 * 128 * 8,
+                                           dtype=torch.int64, device=self.dev)
+            a.stamps = self.step_stamps.data_ptr()
         self.step_args = a
 
     def check_step(self):
@@ -305,7 +313,7 @@ class HipEngine:
         self._heads = self._gemv(w["heads"], self.x, R, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
                                  n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))
         self.plan = plan
-        if self.step is not None:
+        if self.step_cfg is not None:
             self._build_step_args()
         if self._graph is not None:
             _lib.check(self.lib.zmi_graph_destroy(self._graph))
