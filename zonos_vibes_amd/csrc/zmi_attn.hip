@@ -151,12 +151,13 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   }
   __syncthreads();
 
-  const int g_t = t / (256 / G);             // finalising thread -> (head, dims)
-  const int nd = HD / (256 / G);              // dims per thread
-  const int d_t = (t % (256 / G)) * nd;
+  // finalising thread -> (head, dim pair): 64 threads per head, 2 dims each
+  constexpr int TPH = HD / 2;
   if (nch == 1) {
+    if (t >= G * TPH) return;
+    const int g_t = t / TPH, d_t = (t % TPH) * 2;
     const float inv_l = 1.0f / mlv[g_t][1];
-    for (int i = 0; i < nd; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const int d = d_t + i;
       const float o = ((opart[0][g_t][d] + opart[1][g_t][d]) + opart[2][g_t][d]) + opart[3][g_t][d];
       a.out[(size_t)qi * a.ldo + (kh * G + g_t) * HD + d] = (bf16_t)f2bf(o * inv_l);
@@ -168,56 +169,79 @@ __global__ __launch_bounds__(256) void attn_kernel(const AttnArgs a) {
   const size_t pstride = (size_t)G * (HD + 2);
   float* base = a.part + (size_t)blockIdx.x * a.maxch * pstride;
   // write-through (sc1) stores + ticket; the last chunk reads every partial with sc1 loads
-  for (int e = t; e < G * HD; e += 256) {
-    const int g = e / HD, d = e % HD;
-    st_wt(base + c * pstride + g * (HD + 2) + 2 + d,
-          ((opart[0][g][d] + opart[1][g][d]) + opart[2][g][d]) + opart[3][g][d]);
+  for (int e = t; e < G * HD / 2; e += 256) {
+    const int g = e / (HD / 2), d = (e % (HD / 2)) * 2;
+    const float v0 = ((opart[0][g][d] + opart[1][g][d]) + opart[2][g][d]) + opart[3][g][d];
+    const float v1 = ((opart[0][g][d + 1] + opart[1][g][d + 1]) + opart[2][g][d + 1]) + opart[3][g][d + 1];
+    st_wt64(reinterpret_cast<uint64_t*>(base + c * pstride + g * (HD + 2) + 2 + d), pack_f2(v0, v1));
   }
-  if (t < G) {
-    st_wt(base + c * pstride + t * (HD + 2), mlv[t][0]);
-    st_wt(base + c * pstride + t * (HD + 2) + 1, mlv[t][1]);
-  }
+  if (t < G) st_wt64(reinterpret_cast<uint64_t*>(base + c * pstride + t * (HD + 2)), pack_f2(mlv[t][0], mlv[t][1]));
   if (!zmi_last_arriver_wt(a.counters + blockIdx.x, (unsigned)nch, &last_flag)) return;
 
-  // merge: all (m, l) of every chunk in one parallel pass, weights in LDS, then an unrolled,
-  // pipelined pass over the chunk outputs (fixed chunk order: deterministic)
-  __shared__ float mw[MAXCH][G], lw[MAXCH][G], Lsum[G];
-  for (int i = t; i < nch * G; i += 256) {
-    const int cc = i / G, g = i - cc * G;
-    mw[cc][g] = ld_wt(base + cc * pstride + g * (HD + 2));
-    lw[cc][g] = ld_wt(base + cc * pstride + g * (HD + 2) + 1);
-  }
-  __syncthreads();
-  if (t < G) {
+  // merge, one memory round trip: each thread issues the (m, l) pair and its own two output dims of
+  // every chunk as 8-byte sc1 loads before using any of them (pstride and the slab offsets are even,
+  // so both pairs are 8-byte aligned). Accumulation runs in fixed chunk order (deterministic).
+  if (t >= G * TPH) return;
+  const int g_t = t / TPH, d_t = (t % TPH) * 2;
+  const uint64_t* mlp = reinterpret_cast<const uint64_t*>(base + g_t * (HD + 2));
+  const uint64_t* op = reinterpret_cast<const uint64_t*>(base + g_t * (HD + 2) + 2 + d_t);
+  const size_t cs = pstride / 2;  // chunk stride in 8-byte units
+  constexpr int NB = 32;
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+  if (nch <= NB) {
+    uint64_t mlr[NB], orr[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int cc = min(u, nch - 1);  // clamped loads, never used past the end
+      mlr[u] = ld_wt64(mlp + cc * cs);
+      orr[u] = ld_wt64(op + cc * cs);
+    }
     float mmax = -INFINITY;
-    for (int cc = 0; cc < nch; ++cc) mmax = fmaxf(mmax, mw[cc][t]);
-    float L = 0.f;
-    for (int cc = 0; cc < nch; ++cc) {
-      const float w = expf(mw[cc][t] - mmax);
-      mw[cc][t] = w;
-      L += w * lw[cc][t];
-    }
-    Lsum[t] = L;
-  }
-  __syncthreads();
-  float o[HD / (256 / G) > 0 ? HD / (256 / G) : 1];
-  for (int i = 0; i < nd; ++i) o[i] = 0.f;
-  for (int c0 = 0; c0 < nch; c0 += 8) {
-    float v[8][HD / (256 / G) > 0 ? HD / (256 / G) : 1];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int cc = min(c0 + u, nch - 1);  // clamped loads, zero weight past the end
-      for (int i = 0; i < nd; ++i) v[u][i] = ld_wt(base + cc * pstride + g_t * (HD + 2) + 2 + d_t + i);
-    }
+    for (int u = 0; u < NB; ++u)
+      if (u < nch) mmax = fmaxf(mmax, lo_f(mlr[u]));
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float w = (c0 + u < nch) ? mw[c0 + u][g_t] : 0.f;
-      for (int i = 0; i < nd; ++i) o[i] += w * v[u][i];
+    for (int u = 0; u < NB; ++u) {
+      if (u < nch) {
+        const float w = expf(lo_f(mlr[u]) - mmax);
+        L += w * hi_f(mlr[u]);
+        o0 += w * lo_f(orr[u]);
+        o1 += w * hi_f(orr[u]);
+      }
+    }
+  } else {
+    float mmax = -INFINITY;
+    for (int c0 = 0; c0 < nch; c0 += NB) {
+      uint64_t mlr[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) mlr[u] = ld_wt64(mlp + min(c0 + u, nch - 1) * cs);
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+        if (c0 + u < nch) mmax = fmaxf(mmax, lo_f(mlr[u]));
+    }
+    for (int c0 = 0; c0 < nch; c0 += NB) {
+      uint64_t mlr[NB], orr[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int cc = min(c0 + u, nch - 1);
+        mlr[u] = ld_wt64(mlp + cc * cs);
+        orr[u] = ld_wt64(op + cc * cs);
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (c0 + u < nch) {
+          const float w = expf(lo_f(mlr[u]) - mmax);
+          L += w * hi_f(mlr[u]);
+          o0 += w * lo_f(orr[u]);
+          o1 += w * hi_f(orr[u]);
+        }
+      }
     }
   }
-  const float inv_l = 1.0f / Lsum[g_t];
-  for (int i = 0; i < nd; ++i)
-    a.out[(size_t)qi * a.ldo + (kh * G + g_t) * HD + d_t + i] = (bf16_t)f2bf(o[i] * inv_l);
+  const float inv_l = 1.0f / L;
+  bf16_t* dst = a.out + (size_t)qi * a.ldo + (kh * G + g_t) * HD + d_t;
+  dst[0] = (bf16_t)f2bf(o0 * inv_l);
+  dst[1] = (bf16_t)f2bf(o1 * inv_l);
 }
 
 }  // namespace
