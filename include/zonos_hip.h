@@ -177,6 +177,36 @@ int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* 
 int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Prefix conditioner (Zonos.prepare_conditioning, model.py:204-212 -> PrefixConditioner.forward,
+ * conditioning.py:300-310): one output row per conditioning token, then LayerNorm, bf16 out.
+ * Each row names a parameter block and how to produce its d values before the LayerNorm.
+ * ------------------------------------------------------------------------------------- */
+enum {
+  ZMI_COND_EMBED = 0,       /* table[index] (phoneme embedding :233, IntegerConditioner :270)      */
+  ZMI_COND_VECTOR = 1,      /* table[0..d) (learned uncond_vector, conditioning.py:45-46)          */
+  ZMI_COND_FOURIER = 2,     /* [cos f | sin f], f = 2 pi xn @ W^T (FourierConditioner :253-258)     */
+  ZMI_COND_LINEAR = 3,      /* x @ W^T + b (PassthroughConditioner + projection "linear" :24-25)   */
+  ZMI_COND_PASSTHROUGH = 4  /* x (PassthroughConditioner, projection "none")                      */
+};
+typedef struct ZmiCondParam {
+  const void* table;   /* bf16 [rows][d] (EMBED) or [d] (VECTOR)                                */
+  const void* weight;  /* bf16 [d/2][in_dim] (FOURIER) or [d][in_dim] (LINEAR)                  */
+  const void* bias;    /* bf16 [d] (LINEAR) or NULL                                             */
+  int in_dim;          /* input width (<= 256)                                                  */
+  int pad;
+  float min_val, max_val; /* FOURIER input normalisation                                         */
+} ZmiCondParam;
+typedef struct ZmiCondRow {
+  int param;  /* index into the parameter array                                                 */
+  int kind;   /* ZMI_COND_*                                                                      */
+  int index;  /* EMBED row                                                                       */
+  int x_off;  /* offset of this row's inputs in x (FOURIER / LINEAR / PASSTHROUGH)               */
+} ZmiCondRow;
+/* out[r][0..d) = LayerNorm(row r) for r < n_rows; params / rows / x are device arrays. */
+int zmi_prefix_condition(const ZmiCondParam* params, const ZmiCondRow* rows, int n_rows, const float* x, int d,
+                         const void* ln_w, const void* ln_b, float eps, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Synthetic weights: fill with the counter-based uniform stream of zonos_vibes_amd/synthetic.py
  * dtype 0 = bf16, 1 = f32.
  * ------------------------------------------------------------------------------------- */

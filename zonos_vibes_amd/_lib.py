@@ -70,6 +70,18 @@ class StepArgs(ctypes.Structure):
     ]
 
 
+class CondParam(ctypes.Structure):
+    _fields_ = [("table", c_void_p), ("weight", c_void_p), ("bias", c_void_p), ("in_dim", c_int), ("pad", c_int),
+                ("min_val", c_float), ("max_val", c_float)]
+
+
+class CondRow(ctypes.Structure):
+    _fields_ = [("param", c_int), ("kind", c_int), ("index", c_int), ("x_off", c_int)]
+
+
+COND_EMBED, COND_VECTOR, COND_FOURIER, COND_LINEAR, COND_PASSTHROUGH = range(5)
+
+
 _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
@@ -91,6 +103,8 @@ _SIGS = {
     "zmi_dac_conv": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
+    "zmi_prefix_condition": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_float,
+                                     c_void_p, c_void_p]),
     "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),
     "zmi_prefetch": (c_int, [c_void_p, c_int64, c_int, c_void_p]),
     "zmi_graph_begin": (c_int, [c_void_p]),

@@ -11,7 +11,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libzonos_hip.so")
 LIB_STAMPS = os.path.join(HERE, "libzonos_hip_stamps.so")
-SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + [ "zmi_attn.hip", "zmi_sample.hip", "zmi_dac.hip", "zmi_misc.hip",
+SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + [ "zmi_attn.hip", "zmi_sample.hip", "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip",
            "zmi_step.hip"]
 HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_gemv8_impl.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

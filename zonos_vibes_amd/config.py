@@ -7,8 +7,8 @@ written for `Zonos.from_local` (reference `zonos/model.py:65-88`) loads unchange
 * `PrefixConditionerConfig` -> reference `zonos/config.py:42-45`
 * `ZonosConfig.from_dict`   -> reference `zonos/config.py:48-62`
 
-Only the fields the hot path reads are interpreted. The prefix conditioner is out of
-scope; its config is carried through untouched.
+Only the fields the hot path reads are interpreted; the prefix conditioner's list is read by
+`zonos_vibes_amd.conditioning.PrefixConditioner`.
 """
 from __future__ import annotations
 

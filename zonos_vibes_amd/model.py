@@ -17,6 +17,7 @@ import torch
 
 from . import _lib  # noqa: F401  (fail loudly at import if the HIP library is missing)
 from .autoencoder import DACAutoencoder
+from .conditioning import PrefixConditioner
 from .config import N_CODEBOOKS, ZonosConfig
 from .engine import HipEngine, SamplingParams
 
@@ -38,6 +39,9 @@ class Zonos:
         self.step_kernel = step_kernel
         self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill, step_kernel)
         self.autoencoder = autoencoder if autoencoder is not None else DACAutoencoder(device)
+        pcc = config.prefix_conditioner
+        self.prefix_conditioner = (PrefixConditioner(pcc.conditioners, config.backbone.d_model, device, pcc.projection)
+                                   if pcc.conditioners else None)
 
     @property
     def device(self) -> torch.device:
@@ -61,7 +65,10 @@ class Zonos:
         config = ZonosConfig.from_dict(json.load(open(config_path)))
         dac = DACAutoencoder(device, state_dict=load_file(dac_path) if dac_path else None)
         m = cls(config, device, autoencoder=dac, **kw)
-        m.engine.load_state_dict(load_file(model_path))
+        sd = load_file(model_path)
+        m.engine.load_state_dict(sd)
+        if m.prefix_conditioner is not None:
+            m.prefix_conditioner.load_state_dict(sd, prefix="prefix_conditioner.")
         return m
 
     @classmethod
@@ -80,6 +87,13 @@ class Zonos:
                                     max(prefill, e.max_prefill), self.step_kernel)
             self.engine.w = w
             self.engine._build_plan()
+
+    # ------------------------------------------------------------------ conditioning
+    def prepare_conditioning(self, cond_dict: dict, uncond_dict: dict | None = None) -> torch.Tensor:
+        """model.py:204-212: [2, Lc, d] bf16 (conditional rows, then unconditional), one HIP launch."""
+        if self.prefix_conditioner is None:
+            raise ValueError("this config has no prefix conditioners")
+        return self.prefix_conditioner.prepare_conditioning(cond_dict, uncond_dict)
 
     # ------------------------------------------------------------------ generation
     @torch.inference_mode()
