@@ -169,10 +169,20 @@ int zmi_dac_from_codes(const int64_t* codes, int T, const float* codebooks, cons
                        const float* proj_b, void* z, void* stream);
 /* out[t_out][co] = epi( bias + sum_tap sum_ci W[tap][co][ci] * x[t_in][ci] ) with
  *   t_in = q + in_off + tap * tap_step, t_out = q * out_stride + out_phase, q in [0, n_out)
- * epilogue: + skip (fp16, optional), store raw (optional) and/or snake(alpha) (optional). */
+ * epilogue: + skip (fp16, optional), store raw (optional), snake(alpha) (optional) and/or the
+ * raw fp32 value (optional, the encoder's latents). */
 int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* bias, int c_out, int taps,
                  int tap_step, int in_off, int n_out, int out_stride, int out_phase, int t_out, const void* skip,
-                 void* out_raw, void* out_snake, const float* alpha, void* stream);
+                 void* out_raw, void* out_snake, const float* alpha, float* out_f32, void* stream);
+/* DAC encode (DACAutoencoder.encode, autoencoder.py:22-23 -> DacModel.encode, modeling_dac.py:583-608).
+ * col fp16 [T][32] = the 7 taps of encoder.conv1 around each sample (im2col, zero padded). */
+int zmi_dac_im2col7(const float* wav, int t, void* col, void* stream);
+/* residual VQ of latents f32 [T][1024] -> codes int64 [9][T] (modeling_dac.py:283-345, 123-173);
+ * in_w [9][8][1024], in_b [9][8], codebooks [9][1024][8] raw and l2-normalised, codebooks_n2 =
+ * |normalised row|^2 [9][1024], out_w [9][1024][8], out_b [9][1024]; all fp32. */
+int zmi_dac_vq(const float* latents, int t, const float* in_w, const float* in_b, const float* codebooks,
+               const float* codebooks_n, const float* codebooks_n2, const float* out_w, const float* out_b,
+               int64_t* codes, void* stream);
 /* final Snake'd [T][96] -> conv k7 (96->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441)    */
 int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream);
 

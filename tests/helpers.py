@@ -1,5 +1,6 @@
 """Shared test helpers: golden fixture loading and synthetic model construction."""
 import json
+import math
 import os
 
 import torch
@@ -32,3 +33,16 @@ def synthetic_weights(cfg: ZonosConfig, seed=0, zero_eos=False, eos_row_scale=No
 
 def dac_weights(seed=0):
     return dict(syn.iter_torch_cpu(syn.dac_specs(), seed))
+
+
+def synthetic_wav(b: int, n: int, seed: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    t = torch.arange(n, dtype=torch.float64) / 44100.0
+    out = []
+    for _ in range(b):
+        f = 80 + 900 * torch.rand(4, generator=g, dtype=torch.float64)
+        a = 0.2 * torch.rand(4, generator=g, dtype=torch.float64)
+        x = sum(a[i] * torch.sin(2 * math.pi * f[i] * t) for i in range(4))
+        x = x + 0.02 * torch.randn(n, generator=g, dtype=torch.float64)
+        out.append(x.clamp(-0.9, 0.9))
+    return torch.stack(out).unsqueeze(1).float()

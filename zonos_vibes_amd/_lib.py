@@ -101,7 +101,10 @@ _SIGS = {
     "zmi_delay_revert": (c_int, [ctypes.POINTER(Slots), c_int, c_void_p, c_int, c_void_p]),
     "zmi_dac_from_codes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_dac_conv": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                             c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                             c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_dac_im2col7": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    "zmi_dac_vq": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
     "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
     "zmi_prefix_condition": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                      c_void_p, c_void_p]),

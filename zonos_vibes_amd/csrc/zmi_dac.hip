@@ -27,6 +27,7 @@ struct ConvArgs {
   f16_t* out_raw;
   f16_t* out_snake;
   const float* alpha;
+  float* out_f32;
 };
 
 __device__ __forceinline__ float snake(float y, float a) {
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
         o.y = f2h(y[2]) | (f2h(y[3]) << 16);
         *reinterpret_cast<uint2*>(a.out_raw + to * a.c_out + co) = o;
       }
+      if (a.out_f32) *reinterpret_cast<float4*>(a.out_f32 + to * a.c_out + co) = float4{y[0], y[1], y[2], y[3]};
       if (a.out_snake) {
         float z[4];
 #pragma unroll
@@ -160,7 +162,140 @@ __global__ __launch_bounds__(256) void conv_out_kernel(const f16_t* x, int T, in
   out[t] = tanhf(acc + bias);
 }
 
+// encoder.conv1 input (modeling_dac.py:451, Conv1d(1, 64, k7, pad 3)) as a 32-channel im2col row per
+// sample: col[t][k] = wav[t + k - 3] for k < 7 (0 outside the signal), 0 for k >= 7, so the conv runs on
+// the MFMA conv kernel with one tap and c_in = 32
+__global__ __launch_bounds__(256) void im2col7_kernel(const float* wav, int T, f16_t* col) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float v0 = 0.f, v1 = 0.f;
+    const int k0 = 2 * k, k1 = 2 * k + 1;
+    if (k0 < 7 && t + k0 - 3 >= 0 && t + k0 - 3 < T) v0 = wav[t + k0 - 3];
+    if (k1 < 7 && t + k1 - 3 >= 0 && t + k1 - 3 < T) v1 = wav[t + k1 - 3];
+    w[k] = f2h(v0) | (f2h(v1) << 16);
+  }
+  uint4* dst = reinterpret_cast<uint4*>(col + (size_t)t * 32);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dst[i] = uint4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+}
+
+// Residual vector quantizer, one workgroup per frame (modeling_dac.py:283-345 with DacVectorQuantize
+// :123-173): for each of the 9 codebooks, proj = in_proj(r) (8 outputs), e = proj / max(|proj|, 1e-12),
+// score_j = -(|e|^2 - 2 e.cbn_j) + |cbn_j|^2 over the l2-normalised codebook, idx = first argmax,
+// z = proj + (codebook[idx] - proj), r -= out_proj(z). fp32 throughout; latents [T][1024].
+__global__ __launch_bounds__(256) void vq_kernel(const float* lat, int T, const float* in_w, const float* in_b,
+                                                 const float* cb, const float* cbn, const float* cbn2,
+                                                 const float* out_w, const float* out_b, int64_t* codes) {
+  __shared__ float r[1024];
+  __shared__ float proj[8], zq[8];
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int c = t; c < 1024; c += 256) r[c] = lat[(size_t)f * 1024 + c];
+  __syncthreads();
+  for (int i = 0; i < ZMI_NCB; ++i) {
+    // in_proj: wave w -> outputs 2w, 2w+1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 2 * wave + h;
+      const float* wr = in_w + ((size_t)i * 8 + k) * 1024;
+      float s = 0.f;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s += wr[lane + 64 * m] * r[lane + 64 * m];
+      s = wave_sum(s);
+      if (lane == 0) proj[k] = s + in_b[i * 8 + k];
+    }
+    __syncthreads();
+    float p[8], e[8], nrm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      p[k] = proj[k];
+      nrm += p[k] * p[k];
+    }
+    const float den = fmaxf(sqrtf(nrm), 1e-12f);
+    float l2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      e[k] = p[k] / den;
+      l2 += e[k] * e[k];
+    }
+    float best = -INFINITY;
+    int bidx = 0;
+    for (int m = 0; m < 4; ++m) {
+      const int j = t + 256 * m;
+      const float* cr = cbn + ((size_t)i * 1024 + j) * 8;
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dot += e[k] * cr[k];
+      const float sc = -(l2 - 2.f * dot) + cbn2[i * 1024 + j];
+      if (sc > best) {
+        best = sc;
+        bidx = j;
+      }
+    }
+    // block argmax, ties -> lowest index
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float ov = __shfl_xor(best, off);
+      const int oi = __shfl_xor(bidx, off);
+      if (ov > best || (ov == best && oi < bidx)) {
+        best = ov;
+        bidx = oi;
+      }
+    }
+    if (lane == 0) {
+      bv[wave] = best;
+      bi[wave] = bidx;
+    }
+    __syncthreads();
+    if (t == 0) {
+      float bb = bv[0];
+      int ii = bi[0];
+      for (int w = 1; w < 4; ++w)
+        if (bv[w] > bb || (bv[w] == bb && bi[w] < ii)) {
+          bb = bv[w];
+          ii = bi[w];
+        }
+      codes[(size_t)i * T + f] = ii;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) zq[k] = p[k] + (cb[((size_t)i * 1024 + ii) * 8 + k] - p[k]);
+    }
+    __syncthreads();
+    float z[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z[k] = zq[k];
+    for (int c = t; c < 1024; c += 256) {
+      const float* wr = out_w + ((size_t)i * 1024 + c) * 8;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += wr[k] * z[k];
+      r[c] = r[c] - (s + out_b[i * 1024 + c]);
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+extern "C" int zmi_dac_im2col7(const float* wav, int t, void* col, void* stream) {
+  if (t <= 0) return 0;
+  hipLaunchKernelGGL(im2col7_kernel, dim3((t + 255) / 256), dim3(256), 0, (hipStream_t)stream, wav, t, (f16_t*)col);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_dac_vq(const float* latents, int t, const float* in_w, const float* in_b, const float* codebooks,
+                          const float* codebooks_n, const float* codebooks_n2, const float* out_w, const float* out_b,
+                          int64_t* codes, void* stream) {
+  if (t <= 0) return 0;
+  hipLaunchKernelGGL(vq_kernel, dim3(t), dim3(256), 0, (hipStream_t)stream, latents, t, in_w, in_b, codebooks,
+                     codebooks_n, codebooks_n2, out_w, out_b, codes);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
 
 extern "C" int zmi_dac_from_codes(const int64_t* codes, int T, const float* codebooks, const float* proj_w,
                                   const float* proj_b, void* z, void* stream) {
@@ -173,12 +308,13 @@ extern "C" int zmi_dac_from_codes(const int64_t* codes, int T, const float* code
 
 extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* bias, int c_out, int taps,
                             int tap_step, int in_off, int n_out, int out_stride, int out_phase, int t_out,
-                            const void* skip, void* out_raw, void* out_snake, const float* alpha, void* stream) {
+                            const void* skip, void* out_raw, void* out_snake, const float* alpha, float* out_f32,
+                            void* stream) {
   if (c_in % 32) return zmi_fail_msg("dac_conv: c_in % 32");
   if (n_out <= 0) return 0;
   if ((size_t)(n_out - 1) * out_stride + out_phase >= (size_t)t_out) return zmi_fail_msg("dac_conv: output bounds");
   ConvArgs a{(const f16_t*)x, t_in, c_in, (const f16_t*)w, bias, c_out, taps, tap_step, in_off, n_out,
-             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha};
+             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha, out_f32};
   hipStream_t s = (hipStream_t)stream;
   if (c_out % 128 == 0) {
     dim3 grid((n_out + 127) / 128, c_out / 128);

@@ -177,6 +177,40 @@ def dac_specs() -> list[Spec]:
     return out
 
 
+DAC_ENC_HIDDEN = 64
+DAC_ENC_STRIDES = (2, 4, 8, 8)
+
+
+def dac_encoder_specs() -> list[Spec]:
+    """fp32 tensors of the DAC encode path (encoder + quantizer in_proj), DacEncoder modeling_dac.py:444-475,
+    DacEncoderBlock :212-234, DacVectorQuantize.in_proj :119."""
+    out = []
+
+    def conv(name, cout, cin, k):
+        bound = 1.0 / math.sqrt(cin * k)
+        return [Spec(name + ".weight", (cout, cin, k), "f32", bound), Spec(name + ".bias", (cout,), "f32", bound)]
+
+    def snake(name, c):
+        return [Spec(name + ".alpha", (1, c, 1), "f32", 0.25, 1.0)]
+
+    out += conv("encoder.conv1", DAC_ENC_HIDDEN, 1, 7)
+    c = DAC_ENC_HIDDEN
+    for j, s in enumerate(DAC_ENC_STRIDES):
+        p = f"encoder.block.{j}."
+        for u in range(3):
+            q = p + f"res_unit{u + 1}."
+            out += snake(q + "snake1", c) + conv(q + "conv1", c, c, 7)
+            out += snake(q + "snake2", c) + conv(q + "conv2", c, c, 1)
+        out += snake(p + "snake1", c) + conv(p + "conv1", 2 * c, c, 2 * s)
+        c *= 2
+    out += snake("encoder.snake1", c) + conv("encoder.conv2", DAC_LATENT, c, 3)
+    for i in range(N_CODEBOOKS):
+        p = f"quantizer.quantizers.{i}."
+        out += [Spec(p + "in_proj.weight", (DAC_CODEBOOK_DIM, DAC_LATENT, 1), "f32", 1 / math.sqrt(DAC_LATENT)),
+                Spec(p + "in_proj.bias", (DAC_CODEBOOK_DIM,), "f32", 0.1)]
+    return out
+
+
 def materialize_np(spec: Spec, seed: int = 0) -> np.ndarray:
     """numpy array for `spec` (bf16 returned as uint16 bit patterns)."""
     key = tensor_key(seed, spec.name)
