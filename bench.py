@@ -97,6 +97,65 @@ def time_decode_step(model, cond, steps: int = 64):
     return start.elapsed_time(end) * 1000.0 / steps, s_len + lead + steps // 2
 
 
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA
+
+
+def dac_encode_flop_per_frame() -> int:
+    """Algorithmic FLOP of DacEncoder per 512-sample frame (2 x MACs of modeling_dac.py:444-475 at the
+    44.1 kHz dims; the build's 3-tap polyphase strided convs do 1.5x the MACs of those convs)."""
+    macs, t, c = 512 * 64 * 7, 512, 64
+    for s in syn.DAC_ENC_STRIDES:
+        macs += 3 * (c * c * 7 + c * c) * t      # 3 residual units
+        macs += (2 * c) * c * (2 * s) * (t // s)  # strided conv
+        t //= s
+        c *= 2
+    macs += 1024 * c * 3 * t
+    return 2 * macs
+
+
+def time_widened_rows(model, dev):
+    """SURVEY.md §8f rows built this round, measured with HIP events on their own streams (not part of
+    `value`): the prefix conditioner (v0.1 conditioner list, d = 2048, a 40-phoneme utterance) and DAC
+    encode of a 5 s voice-clone prefix (430 frames, BASELINE configs[4])."""
+    from zonos_vibes_amd.conditioning import PrefixConditioner, make_cond_dict, v01_transformer_conditioners
+    d = model.config.backbone.d_model
+    pc = PrefixConditioner(v01_transformer_conditioners(), d, dev)
+    g = torch.Generator().manual_seed(0)
+    pc.load_state_dict({k: (0.02 * torch.randn(sh, generator=g)).to(torch.bfloat16)
+                        for k, sh in pc.param_shapes().items()})
+    cd = make_cond_dict(phonemes="ðɪs ɪz ə bɛntʃmɑːk sɛntəns fɔːɹ ðə pɹɛfɪks kəndɪʃənɚ.",
+                        speaker=torch.zeros(1, 128, dtype=torch.bfloat16), device=dev)
+    out = pc.prepare_conditioning(cd)
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    st.record()
+    for _ in range(reps):
+        pc.prepare_conditioning(cd)
+    en.record()
+    en.synchronize()
+    cond_us = st.elapsed_time(en) * 1000.0 / reps
+    ae = model.autoencoder
+    frames = 430
+    wav = (0.1 * torch.randn(1, 1, frames * DAC_HOP, generator=g)).to(dev)
+    ae.encode(wav)
+    torch.cuda.synchronize()
+    st.record()
+    for _ in range(3):
+        ae.encode(wav)
+    en.record()
+    en.synchronize()
+    enc_s = st.elapsed_time(en) / 1000.0 / 3
+    tflops = dac_encode_flop_per_frame() * frames / enc_s / 1e12
+    return {"prefix_conditioner": {"us_per_utterance": round(cond_us, 1), "rows": int(out.shape[0] * out.shape[1]),
+                                   "note": "host row-table build + one zmi_prefix_condition launch"},
+            "dac_encode": {"frames": frames, "ms": round(enc_s * 1e3, 2),
+                           "frames_per_s": round(frames / enc_s, 1),
+                           "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": MFMA_PEAK_TFLOPS,
+                                        "unit": "TFLOP/s", "frac": round(tflops / MFMA_PEAK_TFLOPS, 4),
+                                        "flop_per_frame": dac_encode_flop_per_frame()}}}
+
+
 def step_bytes(model, pos: int) -> int:
     e = model.engine
     qkv = (e.H + 2 * e.Hkv) * e.hd
@@ -209,6 +268,7 @@ def main():
     # kernel-level measurement (outside the timed region)
     us, bl = time_dominant_kernel(model)
     step_us, step_pos = time_decode_step(model, cond)
+    widened = time_widened_rows(model, dev)
     out = None
     if rank == 0:
         achieved = bl / (us * 1e-6) / 1e9
@@ -233,6 +293,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
+            "widened": widened,
         }
         if world == 1 and not args.no_cpu_baseline:
             sd = {}
