@@ -30,12 +30,12 @@ struct ConvArgs {
   float* out_f32;
 };
 
-__device__ __forceinline__ float snake(float y, float a) {
+__device__ __forceinline__ float snake(float y, float a, float inv_a) {
   // hardware v_sin_f32 (input in revolutions) instead of the libm range-reduced sinf: the epilogue,
   // not the MFMA K loop, bounds the many-sample / few-channel stages, and its error (~1e-6 abs for
   // the |a y| seen here) is far below the fp16 storage rounding that follows
   const float s = __sinf(a * y);
-  return y + (1.0f / (a + 1e-9f)) * (s * s);
+  return y + inv_a * (s * s);  // inv_a = 1 / (a + 1e-9), the reference's reciprocal (modeling_dac.py:97)
 }
 
 template <int WM, int WN>
@@ -119,22 +119,31 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 
 #undef ZMI_CONV_GLOAD
 #undef ZMI_CONV_LSTORE
-  // epilogue: lane holds 4 consecutive output channels of one time step
+  // epilogue: lane holds 4 consecutive output channels of one time step. Channel constants (bias,
+  // Snake alpha and 1 / (alpha + 1e-9)) are loaded / computed once per channel group, outside the
+  // time loop.
 #pragma clang loop unroll(full)
-  for (int j = 0; j < WN; ++j) {
-    const int q = q0 + j * 16 + lr;
-    if (q >= a.n_out) continue;
-    const size_t to = (size_t)q * a.out_stride + a.out_phase;
+  for (int i = 0; i < WM; ++i) {
+    const int co = co0 + i * 16 + kq / 2;  // (lane>>4)*4
+    float bias[4], al[4], ial[4];
 #pragma clang loop unroll(full)
-    for (int i = 0; i < WM; ++i) {
-      const int co = co0 + i * 16 + kq / 2;  // (lane>>4)*4
+    for (int r = 0; r < 4; ++r) {
+      bias[r] = a.bias[co + r];
+      al[r] = a.out_snake ? a.alpha[co + r] : 1.f;
+      ial[r] = 1.0f / (al[r] + 1e-9f);
+    }
+#pragma clang loop unroll(full)
+    for (int j = 0; j < WN; ++j) {
+      const int q = q0 + j * 16 + lr;
+      if (q >= a.n_out) continue;
+      const size_t to = (size_t)q * a.out_stride + a.out_phase;
       float y[4];
       uint2 sk = {0u, 0u};
       if (a.skip) sk = *reinterpret_cast<const uint2*>(a.skip + to * a.c_out + co);
       const uint32_t su[2] = {sk.x, sk.y};
 #pragma clang loop unroll(full)
       for (int r = 0; r < 4; ++r) {
-        y[r] = acc[i][j][r] + a.bias[co + r];
+        y[r] = acc[i][j][r] + bias[r];
         if (a.skip) y[r] = y[r] + h2f(su[r >> 1] >> ((r & 1) * 16));
       }
       if (a.out_raw) {
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
       if (a.out_snake) {
         float z[4];
 #pragma clang loop unroll(full)
-        for (int r = 0; r < 4; ++r) z[r] = snake(y[r], a.alpha[co + r]);
+        for (int r = 0; r < 4; ++r) z[r] = snake(y[r], al[r], ial[r]);
         uint2 o;
         o.x = f2h(z[0]) | (f2h(z[1]) << 16);
         o.y = f2h(z[2]) | (f2h(z[3]) << 16);
