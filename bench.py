@@ -288,7 +288,7 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv8_kernel<W=4,NL=8,MR=2,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": "gemv8_kernel<G=2,W=2,NL=16,MR=2,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",

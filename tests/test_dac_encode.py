@@ -115,3 +115,31 @@ def test_hip_encode_one_second_and_round_trip(weights):
     assert not bad, bad[:5]
     wav2 = ae.decode(codes.cuda())
     assert wav2.shape == (1, 1, 86 * 512) and torch.isfinite(wav2).all()
+
+
+@pytest.mark.gpu
+def test_voice_clone_prefix_flow():
+    """preprocess -> encode -> generate(audio_prefix_codes=...) on the HIP path (BASELINE configs[4] flow):
+    the output starts with the encoded prefix frames (model.py:309-313 keeps them) and matches the
+    oracle's greedy trajectory up to reference near-ties."""
+    from oracle.parity import greedy_divergence
+    from oracle.zonos_cpu import OracleZonos
+    from tests.helpers import synthetic_wav, synthetic_weights
+    from zonos_vibes_amd.config import tiny_transformer
+    from zonos_vibes_amd.model import Zonos
+    cfg = tiny_transformer(2)
+    m = Zonos.synthetic(cfg, "cuda", zero_eos=True, max_seqlen=128, max_prefill=64)
+    wav = synthetic_wav(1, 6 * 512 - 100, 3).cuda()
+    prefix = m.autoencoder.encode(m.autoencoder.preprocess(wav, 44100))
+    assert prefix.shape == (1, 9, 6)
+    g = torch.Generator().manual_seed(4)
+    cond = torch.randn(2, 10, cfg.backbone.d_model, generator=g).to(torch.bfloat16)
+    codes = m.generate(cond.cuda(), audio_prefix_codes=prefix, max_new_tokens=10,
+                       sampling_params=dict(temperature=0.0), progress_bar=False)
+    assert codes.shape == (1, 9, 16)
+    assert torch.equal(codes[..., :6].cpu(), prefix.cpu())
+    om = OracleZonos(cfg, synthetic_weights(cfg, zero_eos=True))
+    info = greedy_divergence(m.engine.delayed[0], om, cond, prefix.cpu(), 10)
+    if info is None:
+        ref = om.generate(cond, prefix.cpu(), max_new_tokens=10, sampling_params=dict(temperature=0.0))
+        assert torch.equal(codes.cpu(), ref)
