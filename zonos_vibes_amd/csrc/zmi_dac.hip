@@ -58,8 +58,13 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   // with the next step's global loads in flight while this step's MFMAs run.
   constexpr int BM = 32 * WM, BN = 32 * WN, KP = 40;
   constexpr int NA = (BM * 4 + 255) / 256, NB = (BN * 4 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) f16_t As[2][BM][KP];
-  __shared__ __attribute__((aligned(16))) f16_t Bs[2][BN][KP];
+  // one LDS block: the double-buffered A/B tiles during the K loop, then (reused) the fp32 output
+  // half-tile [BN/2][BM+4] of the epilogue
+  constexpr int AB_BYTES = 2 * (BM + BN) * KP * 2, TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
+  __shared__ __attribute__((aligned(16))) char lds_raw[AB_BYTES > TILE_BYTES ? AB_BYTES : TILE_BYTES];
+  f16_t(&As)[2][BM][KP] = *reinterpret_cast<f16_t(*)[2][BM][KP]>(lds_raw);
+  f16_t(&Bs)[2][BN][KP] = *reinterpret_cast<f16_t(*)[2][BN][KP]>(lds_raw + 2 * BM * KP * 2);
+  float(&tile)[BN / 2][TP] = *reinterpret_cast<float(*)[BN / 2][TP]>(lds_raw);
   const int tid = threadIdx.x;
   const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
   const int nci = a.c_in / 32, nsteps = a.taps * nci;
@@ -119,50 +124,69 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 
 #undef ZMI_CONV_GLOAD
 #undef ZMI_CONV_LSTORE
-  // epilogue: lane holds 4 consecutive output channels of one time step. Channel constants (bias,
-  // Snake alpha and 1 / (alpha + 1e-9)) are loaded / computed once per channel group, outside the
-  // time loop.
-#pragma clang loop unroll(full)
-  for (int i = 0; i < WM; ++i) {
-    const int co = co0 + i * 16 + kq / 2;  // (lane>>4)*4
-    float bias[4], al[4], ial[4];
-#pragma clang loop unroll(full)
-    for (int r = 0; r < 4; ++r) {
-      bias[r] = a.bias[co + r];
-      al[r] = a.out_snake ? a.alpha[co + r] : 1.f;
-      ial[r] = 1.0f / (al[r] + 1e-9f);
+  // epilogue, in two halves of the time tile (the waves with wn == half own it): the accumulators go
+  // through LDS as an fp32 [t][co] tile, then every thread finishes 8 consecutive channels of one
+  // time row, so the skip loads and the raw / snake / f32 stores are whole 16-32 B per lane and
+  // each row's BM channels are written contiguously.
+  static_assert(WN == 4, "epilogue halves assume 2 x 64 time rows");
+  constexpr int CPR8 = BM / 8, ROWS = BN / 2;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wn == half) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          *reinterpret_cast<f32x4_t*>(&tile[j * 16 + lr][am + i * 16 + kq / 2]) = acc[i][j];
     }
-#pragma clang loop unroll(full)
-    for (int j = 0; j < WN; ++j) {
-      const int q = q0 + j * 16 + lr;
-      if (q >= a.n_out) continue;
-      const size_t to = (size_t)q * a.out_stride + a.out_phase;
-      float y[4];
-      uint2 sk = {0u, 0u};
-      if (a.skip) sk = *reinterpret_cast<const uint2*>(a.skip + to * a.c_out + co);
-      const uint32_t su[2] = {sk.x, sk.y};
-#pragma clang loop unroll(full)
-      for (int r = 0; r < 4; ++r) {
-        y[r] = acc[i][j][r] + bias[r];
-        if (a.skip) y[r] = y[r] + h2f(su[r >> 1] >> ((r & 1) * 16));
-      }
-      if (a.out_raw) {
-        uint2 o;
-        o.x = f2h(y[0]) | (f2h(y[1]) << 16);
-        o.y = f2h(y[2]) | (f2h(y[3]) << 16);
-        *reinterpret_cast<uint2*>(a.out_raw + to * a.c_out + co) = o;
-      }
-      if (a.out_f32) *reinterpret_cast<float4*>(a.out_f32 + to * a.c_out + co) = float4{y[0], y[1], y[2], y[3]};
-      if (a.out_snake) {
-        float z[4];
-#pragma clang loop unroll(full)
-        for (int r = 0; r < 4; ++r) z[r] = snake(y[r], al[r], ial[r]);
-        uint2 o;
-        o.x = f2h(z[0]) | (f2h(z[1]) << 16);
-        o.y = f2h(z[2]) | (f2h(z[3]) << 16);
-        *reinterpret_cast<uint2*>(a.out_snake + to * a.c_out + co) = o;
+    __syncthreads();
+    for (int e = tid; e < ROWS * CPR8; e += 256) {
+      const int row = e / CPR8, c8 = e - row * CPR8;
+      const int q = q_blk + half * ROWS + row;
+      if (q < a.n_out) {
+        const int co = co_blk + c8 * 8;
+        const size_t to = (size_t)q * a.out_stride + a.out_phase;
+        const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(&tile[row][c8 * 8]);
+        const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(&tile[row][c8 * 8 + 4]);
+        float y[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        uint4 sk = {0u, 0u, 0u, 0u};
+        if (a.skip) sk = *reinterpret_cast<const uint4*>(a.skip + to * a.c_out + co);
+        const uint32_t su[4] = {sk.x, sk.y, sk.z, sk.w};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          y[r] = y[r] + a.bias[co + r];
+          if (a.skip) y[r] = y[r] + h2f(su[r >> 1] >> ((r & 1) * 16));
+        }
+        if (a.out_raw) {
+          uint4 o;
+          o.x = f2h(y[0]) | (f2h(y[1]) << 16);
+          o.y = f2h(y[2]) | (f2h(y[3]) << 16);
+          o.z = f2h(y[4]) | (f2h(y[5]) << 16);
+          o.w = f2h(y[6]) | (f2h(y[7]) << 16);
+          *reinterpret_cast<uint4*>(a.out_raw + to * a.c_out + co) = o;
+        }
+        if (a.out_f32) {
+          float4* dst = reinterpret_cast<float4*>(a.out_f32 + to * a.c_out + co);
+          dst[0] = float4{y[0], y[1], y[2], y[3]};
+          dst[1] = float4{y[4], y[5], y[6], y[7]};
+        }
+        if (a.out_snake) {
+          float z[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float al = a.alpha[co + r];
+            z[r] = snake(y[r], al, 1.0f / (al + 1e-9f));
+          }
+          uint4 o;
+          o.x = f2h(z[0]) | (f2h(z[1]) << 16);
+          o.y = f2h(z[2]) | (f2h(z[3]) << 16);
+          o.z = f2h(z[4]) | (f2h(z[5]) << 16);
+          o.w = f2h(z[6]) | (f2h(z[7]) << 16);
+          *reinterpret_cast<uint4*>(a.out_snake + to * a.c_out + co) = o;
+        }
       }
     }
+    __syncthreads();
   }
 }
 
