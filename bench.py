@@ -265,6 +265,21 @@ def main():
     audio_s = frames * DAC_HOP / DAC_SAMPLE_RATE
     rtf = audio_s / elapsed
 
+    # optional end-of-batch gather of every rank's codes to rank 0 (outside the timed
+    # region): int16 payload over RCCL/xGMI
+    gather = None
+    if dist:
+        from zonos_vibes_amd.shard import gather_codes
+        try:
+            g0 = time.perf_counter()
+            got = gather_codes([codes], [rank], world, device=dev)
+            torch.cuda.synchronize()
+            gather = {"ok": True, "ms": round((time.perf_counter() - g0) * 1e3, 2)}
+            if rank == 0:
+                gather["frames_gathered"] = int(sum(c.shape[-1] for c in got))
+        except Exception as exc:  # reported, never fatal to the measurement
+            gather = {"ok": False, "error": f"{type(exc).__name__}: {exc}"[:200]}
+
     # kernel-level measurement (outside the timed region)
     us, bl = time_dominant_kernel(model)
     step_us, step_pos = time_decode_step(model, cond)
@@ -294,6 +309,7 @@ def main():
                          "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "widened": widened,
+            "end_of_batch_gather": gather,
         }
         if world == 1 and not args.no_cpu_baseline:
             sd = {}
