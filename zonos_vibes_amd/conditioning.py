@@ -174,6 +174,8 @@ class PrefixConditioner:
                     cp.table = self.w[p + "int_embedder.weight"].data_ptr()
                 elif t == "FourierConditioner":
                     cp.weight, cp.in_dim = self.w[p + "weight"].data_ptr(), c.get("input_dim", 1)
+                    if cp.in_dim > 256:
+                        raise ValueError("Fourier conditioner input wider than 256")
                 elif t == "PassthroughConditioner":
                     cp.in_dim = c.get("cond_dim") or self.d
                     if c.get("projection", "none") == "linear":

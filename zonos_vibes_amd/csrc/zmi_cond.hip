@@ -53,7 +53,8 @@ __global__ __launch_bounds__(NT) void cond_kernel(const ZmiCondParam* __restrict
   const bf16_t* tab = reinterpret_cast<const bf16_t*>(p.table);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    if (i >= n_my) break;
+    v[i] = 0.f;
+    if (i >= n_my) continue;
     const int j = t + i * NT;
     float y = 0.f;
     switch (kind) {
