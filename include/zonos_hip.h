@@ -61,6 +61,10 @@ typedef struct ZmiGemvArgs {
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
 int64_t zmi_gemv_slab_floats(int M, int N, int K, int ksplit); /* ksplit <= 0: library plan */
+/* out[r] = LayerNorm(x[r]) bf16 for r < m (nn.LayerNorm at _torch.py:88,90; same formula as the GEMV
+ * prologue). The prefill normalises each layer input once, then runs the plain GEMMs on it. */
+int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps, void* out,
+                       int ldo, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Attention: GQA scaled-dot-product attention over the KV cache, one query position per

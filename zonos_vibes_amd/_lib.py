@@ -86,6 +86,8 @@ _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
     "zmi_gemv_slab_floats": (c_int64, [c_int, c_int, c_int, c_int]),
+    "zmi_layernorm_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
+                                   c_void_p]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),

@@ -130,6 +130,7 @@ class HipEngine:
             self.params = z(S * ctypes.sizeof(_lib.Sampling), dt=torch.uint8)
             P = self.max_prefill
             self.x_pre, self.q_pre, self.attn_pre = z(2 * P, d), z(2 * P, qd), z(2 * P, qd)
+            self.xn_pre = z(2 * P, d)  # LayerNorm'd prefill rows (zmi_layernorm_rows)
             self.h_pre = z(2 * P, self.F)
             self.row_kv_pre = z(2 * P, dt=torch.int32)
             self.row_pos_pre = z(2 * P, dt=torch.int32)
@@ -428,14 +429,19 @@ class HipEngine:
     def _prefill_layers(self, m: int, max_pos: int):
         d, qd = self.d, self.H * self.hd
         qkv_n = (self.H + 2 * self.Hkv) * self.hd
+        def ln(wb):  # normalise the m prefill rows once; the GEMMs below take them plain
+            _lib.check(self.lib.zmi_layernorm_rows(self.x_pre.data_ptr(), d, m, d, wb[0].data_ptr(), wb[1].data_ptr(),
+                                                   self.eps, self.xn_pre.data_ptr(), d, self.sptr), "layernorm")
+            return self.xn_pre
+
         for i, lw in enumerate(self.w["layers"]):
-            self._run_gemv(self._gemv(lw["qkv"], self.x_pre, m, qkv_n, d, _lib.EPI_QKV, self.q_pre, qd,
-                                      ln=(lw["ln1_w"], lw["ln1_b"]), kv=(self.kc[i], self.vc[i]),
+            self._run_gemv(self._gemv(lw["qkv"], ln((lw["ln1_w"], lw["ln1_b"])), m, qkv_n, d, _lib.EPI_QKV,
+                                      self.q_pre, qd, kv=(self.kc[i], self.vc[i]),
                                       row_kv=self.row_kv_pre, row_pos=self.row_pos_pre, ksplit=1))
             self._attention(i, self.q_pre, m, self.row_kv_pre, self.row_pos_pre, max_pos, self.attn_pre)
             self._run_gemv(self._gemv(lw["out"], self.attn_pre, m, d, qd, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
-            self._run_gemv(self._gemv(lw["fc1"], self.x_pre, m, 2 * self.F, d, _lib.EPI_SWIGLU, self.h_pre, self.F,
-                                      ln=(lw["ln2_w"], lw["ln2_b"]), ksplit=1))
+            self._run_gemv(self._gemv(lw["fc1"], ln((lw["ln2_w"], lw["ln2_b"])), m, 2 * self.F, d, _lib.EPI_SWIGLU,
+                                      self.h_pre, self.F, ksplit=1))
             self._run_gemv(self._gemv(lw["fc2"], self.h_pre, m, d, self.F, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
 
     # ------------------------------------------------------------------ readback
