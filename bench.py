@@ -156,6 +156,35 @@ def time_widened_rows(model, dev):
                                         "flop_per_frame": dac_encode_flop_per_frame()}}}
 
 
+def utterance_breakdown(model, cond, n_new: int, chunk: int = 128) -> dict:
+    """Wall time of one more C2 utterance split into phases (host clock, each phase bracketed by a
+    stream synchronisation; not part of `value`)."""
+    from zonos_vibes_amd.engine import SamplingParams
+    e = model.engine
+    params = SamplingParams(temperature=0.0, cfg_scale=2.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.prefill(0, cond, None, n_new, params)
+    e.stream.synchronize()
+    t1 = time.perf_counter()
+    steps = 0
+    while steps < n_new + 8:
+        n = min(chunk, n_new + 8 - steps)
+        e.step(n)
+        steps += n
+        if not e.slot_state(0)["active"]:
+            break
+    t2 = time.perf_counter()
+    codes = e.read_codes(0)
+    e.release(0)
+    t3 = time.perf_counter()
+    model.autoencoder.decode(codes)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    return {"prefill_ms": round((t1 - t0) * 1e3, 2), "decode_loop_ms": round((t2 - t1) * 1e3, 2),
+            "readback_ms": round((t3 - t2) * 1e3, 2), "dac_decode_ms": round((t4 - t3) * 1e3, 2)}
+
+
 def step_bytes(model, pos: int) -> int:
     e = model.engine
     qkv = (e.H + 2 * e.Hkv) * e.hd
@@ -284,6 +313,7 @@ def main():
     us, bl = time_dominant_kernel(model)
     step_us, step_pos = time_decode_step(model, cond)
     widened = time_widened_rows(model, dev)
+    breakdown = utterance_breakdown(model, cond, n_new)
     out = None
     if rank == 0:
         achieved = bl / (us * 1e-6) / 1e9
@@ -308,6 +338,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
+            "utterance_breakdown": breakdown,
             "widened": widened,
             "end_of_batch_gather": gather,
         }
