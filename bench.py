@@ -47,7 +47,7 @@ def time_dominant_kernel(model, reps: int = 3):
     Infinity Cache, so the bytes come from HBM as in the decode step.
     """
     e = model.engine
-    items = [item for kind, item in e.plan if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
+    items = [item for kind, item in e._plan(2) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(e.stream):
         for it in items:
@@ -60,7 +60,7 @@ def time_dominant_kernel(model, reps: int = 3):
     end.synchronize()
     n = reps * len(items)
     us = start.elapsed_time(end) * 1000.0 / n
-    bytes_launch = 2 * e.F * e.d * 2 + e.R * e.d * 2 + e.R * e.F * 2 + 2 * e.d * 2
+    bytes_launch = 2 * e.F * e.d * 2 + 2 * e.d * 2 + 2 * e.F * 2 + 2 * e.d * 2
     return us, bytes_launch
 
 
@@ -85,11 +85,11 @@ def time_decode_step(model, cond, steps: int = 64):
     params = SamplingParams(temperature=0.0, cfg_scale=2.0)
     s_len = e.prefill(0, cond, None, N_NEW, params)
     lead = max(0, N_NEW // 2 - steps // 2)
-    e.step(lead)
+    e.step(lead, slots=1)
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(e.stream):
         start.record(e.stream)
-        e.step(steps)
+        e.step(steps, slots=1)
         end.record(e.stream)
     end.synchronize()
     assert e.slot_state(0)["active"], "slot finished inside the timed decode window"
@@ -170,7 +170,7 @@ def utterance_breakdown(model, cond, n_new: int, chunk: int = 128) -> dict:
     steps = 0
     while steps < n_new + 8:
         n = min(chunk, n_new + 8 - steps)
-        e.step(n)
+        e.step(n, slots=1)
         steps += n
         if not e.slot_state(0)["active"]:
             break
@@ -189,7 +189,7 @@ def step_bytes(model, pos: int) -> int:
     e = model.engine
     qkv = (e.H + 2 * e.Hkv) * e.hd
     w = e.L * 2 * (qkv * e.d + e.d * e.H * e.hd + 2 * e.F * e.d + e.d * e.F) + 9 * 1025 * e.d * 2
-    kv = e.R * e.L * e.Hkv * e.hd * 2 * 2 * (pos + 1)
+    kv = 2 * e.L * e.Hkv * e.hd * 2 * 2 * (pos + 1)
     return w + kv
 
 
@@ -333,7 +333,7 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv8_kernel<G=2,W=2,NL=16,MR=2,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": "gemv_kernel<G=2,W=2,NL=16,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",

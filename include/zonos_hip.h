@@ -35,11 +35,11 @@ enum {
 enum { ZMI_PACK_IDENTITY = 0, ZMI_PACK_SWIGLU = 1 };
 
 typedef struct ZmiGemvArgs {
-  const void* W;        /* packed weight (zmi_pack_weight)                                    */
+  const void* W;        /* packed weight (zmi_pack_weight, layout M8)                          */
   const void* X;        /* bf16 [M][ldx] activations                                          */
-  int M, N, K, ldx;     /* N = packed (padded) columns, multiple of 16; K multiple of 128       */
-  int ksplit;           /* <= 0: library plan (depends on N, K only)                           */
-  int nchunk;           /* filled by the library                                               */
+  int M, N, K, ldx;     /* N = packed (padded) columns, multiple of 8; K in {512 .. 8192}, pow2  */
+  int groups;           /* 8-column groups per workgroup: 0 = library choice, else 1 or 2      */
+  int reserved;
   const void* ln_w;     /* bf16 [K] LayerNorm weight, or NULL for a plain GEMV                */
   const void* ln_b;     /* bf16 [K] LayerNorm bias                                             */
   float eps;
@@ -48,78 +48,30 @@ typedef struct ZmiGemvArgs {
   int n_valid;          /* real (unpadded) columns                                             */
   const int* row_kv;    /* QKV: [M] KV-cache row of each activation row                        */
   const int* row_pos;   /* QKV: [M] position (<0: inactive row, nothing written)               */
-  void* k_cache;        /* QKV: bf16 [rows][hkv][smax][hd] for this layer                      */
-  void* v_cache;
+  void* k_cache;        /* QKV: bf16 K cache [rows][hkv][smax][hd] of this layer               */
+  void* v_cache;        /* QKV: bf16 V cache, transposed: [rows][hkv][hd][smax]                 */
   int smax, hq, hkv, hd;
   const float* rope;    /* [16384][hd/2][2] (cos, sin) fp32 (_torch.py:9-15)                  */
-  float* slab;          /* split-K workspace                                                   */
-  unsigned* counters;   /* split-K arrival tickets, zero-initialised, re-armed by the kernel   */
-  int64_t slab_cap;     /* floats available at `slab` (checked before launch)                  */
-  int64_t counters_cap; /* tickets available at `counters` (checked before launch)             */
 } ZmiGemvArgs;
 
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
+/* One kernel for every M: a row's result is bit-identical whatever the batch it is computed in. */
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
-int64_t zmi_gemv_slab_floats(int M, int N, int K, int ksplit); /* ksplit <= 0: library plan */
-/* out[r] = LayerNorm(x[r]) bf16 for r < m (nn.LayerNorm at _torch.py:88,90; same formula as the GEMV
- * prologue). The prefill normalises each layer input once, then runs the plain GEMMs on it. */
-int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps, void* out,
-                       int ldo, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Attention: GQA scaled-dot-product attention over the KV cache, one query position per
  * (query row). Replaces F.scaled_dot_product_attention(q, k, v, is_causal, enable_gqa)
  * at zonos/backbone/_torch.py:136 for decode (1 query) and prefill (causal = position bound).
  * ------------------------------------------------------------------------------------- */
-/* q_kv_row may be NULL: query i then reads KV-cache row i (the decode layout). */
+/* K cache [rows][hkv][smax][hd], V cache transposed [rows][hkv][hd][smax] (bf16, as the QKV
+ * epilogue writes them). q_kv_row may be NULL: query i then reads KV-cache row i (decode). Softmax in the
+ * 512-key block structure of the reference's CPU kernel (probabilities rounded to bf16 before P.V).
+ * `work` holds zmi_attention_work_bytes(n_query, hq, hkv, hd, max_pos) zero-initialised bytes,
+ * re-armed by every launch; its first 4 bytes become nonzero if a cross-block hand-off timed out. */
 int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                   const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
-                  int ldo, float* partials, unsigned* counters, void* stream);
-int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
-
-/* ---------------------------------------------------------------------------------------
- * Persistent decode step: the whole backbone (26 x [LayerNorm -> QKV + RoPE + KV write ->
- * attention -> out_proj + residual -> LayerNorm -> fc1 + SwiGLU -> fc2 + residual]), norm_f
- * and the 9 heads in ONE launch of one 1024-thread workgroup per CU. Replaces
- * TorchZonosBackbone.forward (zonos/backbone/_torch.py:73-152) + _compute_logits
- * (zonos/model.py:100-116, before CFG) for one decode position of every row.
- * Each wave runs a static list of weight-slice tasks (host-built, zonos_vibes_amd/step_plan.py)
- * and issues a task's weights before it waits for the task's input, so the weight stream runs
- * ahead of the layer's dependency chain; activations move between CUs as 8-byte
- * {tag, value} granules (MI355X_MICROARCH.md, R2 hand-off). GEMV arithmetic is bit-identical
- * to zmi_gemv_launch's decode kernel.
- * ------------------------------------------------------------------------------------- */
-typedef struct ZmiStepLayer {
-  const void *ln1_w, *ln1_b, *ln2_w, *ln2_b; /* bf16 [d]                                       */
-  const void *qkv, *out, *fc1, *fc2;         /* packed weights (zmi_pack_weight; fc1 SWIGLU)     */
-  void *k_cache, *v_cache;                   /* bf16 [rows][hkv][smax][hd] of this layer          */
-} ZmiStepLayer;
-
-typedef struct ZmiStepArgs {
-  const ZmiStepLayer* layers;  /* device [n_layer]                                            */
-  const uint32_t* tasks;       /* device task words (step_plan.py)                            */
-  const int32_t* task_hdr;     /* device [n_blocks][4] = layer_off, layer_len, head_off, head_len */
-  const void* x;               /* bf16 [rows][d] step input (next-step embedding)             */
-  const int* row_pos;          /* [rows] position, < 0 = inactive row                          */
-  const float* rope;           /* [16384][hd/2][2]                                             */
-  const void* heads;           /* packed [9248][d]                                             */
-  const void *nf_w, *nf_b;     /* norm_f                                                       */
-  float* logits;               /* f32 [rows][9][1026]                                          */
-  uint64_t* granules;          /* zmi_step_granule_words(rows, ...) words, zero-initialised    */
-  uint32_t* ctl;               /* 4 words: epoch (init 1), finish ticket, error, spare          */
-  uint64_t* stamps;            /* NULL; diagnostic build (-DZMI_STAMPS) timestamps               */
-  int rows, n_layer, smax, n_blocks, att_cus, att_pmax;
-  float eps;
-  int tokens;                  /* weight slices in transit per CU (0 = default 16)              */
-} ZmiStepArgs;
-
-/* granule words the step kernel needs for `rows` rows */
-int64_t zmi_step_granule_words(int rows, int n_blocks, int n_layer);
-/* dynamic LDS bytes of one workgroup, or -1 if the configuration does not fit */
-int64_t zmi_step_lds_bytes(int rows, int att_pmax);
-/* CUs of the current device that can each hold one step workgroup (0 = cannot run) */
-int zmi_step_blocks(int rows, int att_pmax);
-int zmi_step_launch(const ZmiStepArgs* args, void* stream);
+                  int ldo, void* work, void* stream);
+int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 
 /* ---------------------------------------------------------------------------------------
  * Sampler + EOS state machine + delay-pattern frame write, per utterance slot.
@@ -234,9 +186,6 @@ int zmi_graph_begin(void* stream);
 int zmi_graph_end(void* stream, void** graph_exec);
 int zmi_graph_launch(void* graph_exec, int times, void* stream);
 int zmi_graph_destroy(void* graph_exec);
-
-/* Stream [p, p + bytes) through the memory side (Infinity Cache warm-up for a later kernel). */
-int zmi_prefetch(const void* p, int64_t bytes, int blocks, void* stream);
 
 const char* zmi_last_error(void);
 int zmi_version(void);

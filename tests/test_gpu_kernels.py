@@ -24,32 +24,27 @@ def stream_ptr():
 def pack(W, mode=0, n_pad=None):
     L = _lib()
     n, k = W.shape
-    n_pad = n_pad or (n + 15) // 16 * 16
+    n_pad = n_pad or (n + 7) // 8 * 8
     out = torch.empty(n_pad * k, dtype=torch.bfloat16, device=DEV)
     L.check(L.lib().zmi_pack_weight(W.data_ptr(), out.data_ptr(), n, k, n_pad, mode, stream_ptr()))
     return out, n_pad
 
 
-def gemv(W, X, epi, out, ldo, n_valid=None, ln=None, ksplit=0, mode=0, extra=None):
+def gemv(W, X, epi, out, ldo, n_valid=None, ln=None, mode=0, extra=None, groups=0, packed=None):
     L = _lib()
-    Wp, n_pad = pack(W, mode)
+    Wp, n_pad = packed if packed is not None else pack(W, mode)
     M, K = X.shape
     a = L.GemvArgs()
     a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), X.data_ptr(), M, n_pad, K, K
-    a.ksplit = ksplit
+    a.groups = groups
     if ln is not None:
         a.ln_w, a.ln_b, a.eps = ln[0].data_ptr(), ln[1].data_ptr(), 1e-5
     a.out, a.ldo = out.data_ptr(), ldo
     a.n_valid = W.shape[0] if n_valid is None else n_valid
-    slab = torch.zeros(max(L.lib().zmi_gemv_slab_floats(M, n_pad, K, ksplit), 1), dtype=torch.float32, device=DEV)
-    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
-    a.slab, a.counters = slab.data_ptr(), cnt.data_ptr()
-    a.slab_cap, a.counters_cap = slab.numel(), cnt.numel()
     if extra:
         extra(a)
     L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), epi, stream_ptr()), "gemv")
     torch.cuda.synchronize()
-    assert int(cnt.abs().sum()) == 0, "split-K tickets must be re-armed"
     return out
 
 
@@ -58,8 +53,8 @@ def rnd(*shape, scale=1.0, seed=0):
     return (torch.rand(*shape, generator=g) * 2 - 1).mul(scale).to(torch.bfloat16).to(DEV)
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 64, 256), (2, 3072, 2048), (5, 2048, 8192), (8, 9248, 2048), (16, 256, 512),
-                                   (33, 512, 1024), (130, 256, 2048), (2, 2048, 8192), (1, 512, 512)])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 512), (2, 3072, 2048), (5, 2048, 8192), (8, 9248, 2048), (16, 256, 512),
+                                   (33, 512, 1024), (130, 256, 2048), (2, 2048, 8192), (1, 512, 4096), (19, 136, 8192)])
 def test_gemv_f32_sums_match_fp64(M, N, K):
     L = _lib()
     W, X = rnd(N, K, scale=0.05, seed=1), rnd(M, K, seed=2)
@@ -70,19 +65,29 @@ def test_gemv_f32_sums_match_fp64(M, N, K):
     assert ((out.double() - ref).abs() <= bound).all()
 
 
-@pytest.mark.parametrize("big,smalls", [(8, (1, 2, 7)), (40, (9, 17))])
-def test_gemv_is_batch_invariant(big, smalls):
-    """Rows are bit-identical whatever the batch, within a kernel regime: the decode kernel takes
-    every M <= 8 (zmi_gemv8_impl.h), the MFMA strip kernel every larger M."""
+@pytest.mark.parametrize("K,ln", [(2048, True), (2048, False), (8192, False), (512, True)])
+def test_gemv_is_batch_invariant(K, ln):
+    """A row's result is bit-identical whatever batch it is computed in (any M, any row tile,
+    any position inside the tile): SURVEY.md §0.3, the reference's batch_size=1 semantics."""
     L = _lib()
-    W = rnd(1024, 2048, scale=0.05, seed=3)
-    X = rnd(big, 2048, seed=4)
-    ref = torch.zeros(big, 1024, dtype=torch.float32, device=DEV)
-    gemv(W, X, L.EPI_F32, ref, 1024)
-    for m in smalls:
-        small = torch.zeros(m, 1024, dtype=torch.float32, device=DEV)
-        gemv(W, X[:m].contiguous(), L.EPI_F32, small, 1024)
-        assert torch.equal(small, ref[:m])
+    N = 1024
+    W = rnd(N, K, scale=0.05, seed=3)
+    big = 130
+    X = rnd(big, K, scale=2.0, seed=4)
+    lnp = (rnd(K, scale=0.1, seed=10) + 1, rnd(K, scale=0.02, seed=11)) if ln else None
+    packed = pack(W)
+    ref = torch.zeros(big, N, dtype=torch.float32, device=DEV)
+    gemv(W, X, L.EPI_F32, ref, N, ln=lnp, packed=packed)
+    for lo, hi in [(0, 1), (0, 2), (5, 12), (0, 16), (3, 20), (17, 50), (64, 130), (129, 130)]:
+        small = torch.zeros(hi - lo, N, dtype=torch.float32, device=DEV)
+        gemv(W, X[lo:hi].contiguous(), L.EPI_F32, small, N, ln=lnp, packed=packed)
+        assert torch.equal(small, ref[lo:hi]), (lo, hi)
+    # the column-group choice (2 groups per block are built for the LayerNorm'd K = 2048 shape)
+    # does not change a column's arithmetic either
+    for g in ((1, 2) if (K, ln) == (2048, True) else (1,)):
+        alt = torch.zeros(big, N, dtype=torch.float32, device=DEV)
+        gemv(W, X, L.EPI_F32, alt, N, ln=lnp, packed=packed, groups=g)
+        assert torch.equal(alt, ref)
 
 
 def _ulp_close(a, b, ulps=1):
@@ -128,7 +133,7 @@ def test_gemv_qkv_rope_kv_write():
     W, X = rnd(n, d, scale=0.05, seed=12), rnd(2, d, seed=13)
     rope = rope_table(hd).to(DEV)
     kc = torch.zeros(2, Hkv, smax, hd, dtype=torch.bfloat16, device=DEV)
-    vc = torch.zeros_like(kc)
+    vc = torch.zeros(2, Hkv, hd, smax, dtype=torch.bfloat16, device=DEV)
     q = torch.zeros(2, H * hd, dtype=torch.bfloat16, device=DEV)
     row_kv = torch.tensor([0, 1], dtype=torch.int32, device=DEV)
     row_pos = torch.tensor([5, 37], dtype=torch.int32, device=DEV)
@@ -146,33 +151,99 @@ def test_gemv_qkv_rope_kv_write():
         kr = oz.apply_rope(kk.view(1, 1, 1, hd), fc[p:p + 1].unsqueeze(0)).view(-1)
         assert _ulp_close(q[r], qr, 2) > 0.995
         assert _ulp_close(kc[r, 0, p], kr, 2) > 0.995
-        assert _ulp_close(vc[r, 0, p], vv, 1) > 0.995
-        assert kc[r, 0, :p].abs().sum() == 0
+        assert _ulp_close(vc[r, 0, :, p], vv, 1) > 0.995  # V cache is stored transposed [hd][position]
+        assert kc[r, 0, :p].abs().sum() == 0 and vc[r, 0, :, :p].abs().sum() == 0
 
 
-@pytest.mark.parametrize("positions", [(0, 1), (63, 64), (65, 200), (511, 7)])
-def test_attention_matches_sdpa(positions):
+def _attention(q, kc, vc, positions, kv_rows=None, hq=16, hkv=4):
+    """Run zmi_attention; kc [R][hkv][smax][hd], vc the same cache in the kernel's transposed layout."""
     L = _lib()
-    H, Hkv, hd, smax = 16, 4, 128, 512
+    hd, smax = kc.shape[-1], kc.shape[-2]
+    n = len(positions)
+    vt = vc.transpose(-1, -2).contiguous()
+    out = torch.zeros(n, hq * hd, dtype=torch.bfloat16, device=DEV)
+    rp = torch.tensor(positions, dtype=torch.int32, device=DEV)
+    rk = None if kv_rows is None else torch.tensor(kv_rows, dtype=torch.int32, device=DEV)
+    work = torch.zeros(L.lib().zmi_attention_work_bytes(n, hq, hkv, hd, smax - 1), dtype=torch.uint8, device=DEV)
+    for _ in range(2):  # the second launch checks that the hand-off state re-armed itself
+        L.check(L.lib().zmi_attention(q.data_ptr(), hq * hd, kc.data_ptr(), vt.data_ptr(), _lib().ptr(rk),
+                                      rp.data_ptr(), n, hq, hkv, hd, smax, smax - 1, out.data_ptr(), hq * hd,
+                                      work.data_ptr(), stream_ptr()))
+        torch.cuda.synchronize()
+        assert int(work[:4].view(torch.int32).item()) == 0, "cross-block hand-off timed out"
+    return out
+
+
+def _check_attention(out, q, kc, vc, positions, kv_rows=None, hq=16, hkv=4):
+    from oracle.attention_cpu import attend
+    hd = kc.shape[-1]
+    for r, p in enumerate(positions):
+        kr = r if kv_rows is None else kv_rows[r]
+        qq = q[r].view(hq, hd).cpu()
+        got = out[r].view(hq, hd).float().cpu()
+        ref = attend(qq, kc[kr].cpu(), vc[kr].cpu(), p).float()
+        # same blocking and rounding points: equal up to the fp32 accumulation order, which can
+        # flip a probability's bf16 rounding (then ~1 bf16 ulp of the output)
+        ulp = torch.ldexp(torch.ones_like(ref), torch.frexp(ref.abs().clamp_min(1e-6))[1] - 8)
+        err = (got - ref).abs()
+        assert (err <= 2 * ulp + 1e-4).float().mean() > 0.995, (p, err.max().item())
+        assert err.max() < 2e-2, (p, err.max().item())
+        # and against plain fp32 SDPA, the math the op stands for
+        sd = F.scaled_dot_product_attention(qq.float().view(1, hq, 1, hd), kc[kr, :, : p + 1].float().cpu().unsqueeze(0),
+                                            vc[kr, :, : p + 1].float().cpu().unsqueeze(0), enable_gqa=True).view(hq, hd)
+        assert (got - sd).abs().max() < 2e-2, p
+
+
+@pytest.mark.parametrize("positions", [(0, 1), (63, 64), (65, 200), (511, 7), (512, 513), (1023, 1500)])
+def test_attention_matches_reference_blocking(positions):
+    H, Hkv, hd, smax = 16, 4, 128, 2048
     R = len(positions)
     kc = rnd(R, Hkv, smax, hd, seed=20)
     vc = rnd(R, Hkv, smax, hd, seed=21)
-    q = rnd(R, H * hd, seed=22)
-    out = torch.zeros(R, H * hd, dtype=torch.bfloat16, device=DEV)
-    rk = torch.arange(R, dtype=torch.int32, device=DEV)
-    rp = torch.tensor(positions, dtype=torch.int32, device=DEV)
-    part = torch.zeros(L.lib().zmi_attention_partial_floats(R, H, Hkv, hd, smax - 1), device=DEV)
-    cnt = torch.zeros(R * Hkv, dtype=torch.int32, device=DEV)
-    L.check(L.lib().zmi_attention(q.data_ptr(), H * hd, kc.data_ptr(), vc.data_ptr(), rk.data_ptr(), rp.data_ptr(), R,
-                                  H, Hkv, hd, smax, smax - 1, out.data_ptr(), H * hd, part.data_ptr(), cnt.data_ptr(),
-                                  stream_ptr()))
-    torch.cuda.synchronize()
-    for r, p in enumerate(positions):
-        qq = q[r].view(1, H, 1, hd).float().cpu()
-        k = kc[r, :, : p + 1].unsqueeze(0).float().cpu()
-        v = vc[r, :, : p + 1].unsqueeze(0).float().cpu()
-        ref = F.scaled_dot_product_attention(qq, k, v, enable_gqa=True).view(-1)
-        assert (out[r].float().cpu() - ref).abs().max() < 1e-2
+    q = rnd(R, H * hd, scale=2.0, seed=22)
+    out = _attention(q, kc, vc, positions)
+    _check_attention(out, q, kc, vc, positions)
+
+
+def test_attention_long_context_c5_positions():
+    """C5 voice-clone lengths: P = 430 prefix frames + 5168 new ones reach ~5.8k positions, 12
+    blocks of 512 keys chained through the cross-block maxima and merged in block order."""
+    H, Hkv, hd, smax = 16, 4, 128, 5784
+    positions = (2047, 2049, 4100, 5775)
+    R = len(positions)
+    kc = rnd(R, Hkv, smax, hd, seed=30)
+    vc = rnd(R, Hkv, smax, hd, seed=31)
+    q = rnd(R, H * hd, scale=3.0, seed=32)
+    out = _attention(q, kc, vc, positions)
+    _check_attention(out, q, kc, vc, positions)
+
+
+def test_attention_prefill_rows_with_kv_table():
+    """Prefill layout: 2 x S query rows, each its own position, reading the KV row of its CFG half."""
+    H, Hkv, hd, smax = 4, 1, 128, 640
+    S = 600
+    kc = rnd(2, Hkv, smax, hd, seed=40)
+    vc = rnd(2, Hkv, smax, hd, seed=41)
+    pos = [p for p in range(S)] * 2
+    rows = [0] * S + [1] * S
+    q = rnd(2 * S, H * hd, seed=42)
+    out = _attention(q, kc, vc, pos, kv_rows=rows, hq=H, hkv=Hkv)
+    pick = [0, 1, 300, 511, 512, 599, S, S + 513, 2 * S - 1]
+    _check_attention(out[pick], q[pick], kc, vc, [pos[i] for i in pick], kv_rows=[rows[i] for i in pick], hq=H,
+                     hkv=Hkv)
+
+
+def test_attention_is_batch_invariant():
+    H, Hkv, hd, smax = 16, 4, 128, 1200
+    positions = [5, 700, 1100, 64, 513, 1000, 999, 2]
+    R = len(positions)
+    kc = rnd(R, Hkv, smax, hd, seed=50)
+    vc = rnd(R, Hkv, smax, hd, seed=51)
+    q = rnd(R, H * hd, seed=52)
+    full = _attention(q, kc, vc, positions)
+    for r in (0, 1, 5):
+        one = _attention(q[r:r + 1].contiguous(), kc[r:r + 1].contiguous(), vc[r:r + 1].contiguous(), positions[r:r + 1])
+        assert torch.equal(one[0], full[r])
 
 
 def _slots(S=4, tcap=64):

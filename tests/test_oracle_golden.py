@@ -79,3 +79,41 @@ def test_dac_decode_matches_transformers():
     wav = OracleDAC(dac_weights()).decode(t["codes"])
     assert wav.shape == t["wav"].shape
     torch.testing.assert_close(wav, t["wav"], rtol=0, atol=1e-6)
+
+
+def test_attention_block_structure_matches_torch_cpu_sdpa():
+    """oracle/attention_cpu.py restates the softmax blocking of the reference's attention op
+    (F.scaled_dot_product_attention on bf16 CPU tensors, _torch.py:136): 512-key blocks with the
+    probabilities rounded to bf16 reproduce torch's output far more often than fp32 probabilities
+    or an unblocked softmax do. The residue is the fp32 accumulation order of its GEMMs."""
+    import torch.nn.functional as F
+    from oracle.attention_cpu import attend_row
+    torch.manual_seed(0)
+    torch.set_num_threads(4)
+    S = 700
+    q = torch.randn(1, 16, 1, 128).to(torch.bfloat16)
+    k = torch.randn(1, 4, S, 128).to(torch.bfloat16)
+    v = torch.randn(1, 4, S, 128).to(torch.bfloat16)
+    ref = F.scaled_dot_product_attention(q, k, v, enable_gqa=True)[0, :, 0]
+
+    def frac(**kw):
+        got = torch.stack([attend_row(q[0, h, 0], k[0, h // 4], v[0, h // 4], **kw) for h in range(16)])
+        return (got == ref).float().mean().item()
+
+    blocked = frac()
+    assert blocked > 0.78
+    assert blocked > frac(round_p=False) + 0.1
+    assert blocked > frac(block=1 << 20) + 0.02
+    # causal prefill rows follow the same per-query structure
+    Sp = 540
+    qp = torch.randn(1, 4, Sp, 128).to(torch.bfloat16)
+    kp = torch.randn(1, 1, Sp, 128).to(torch.bfloat16)
+    vp = torch.randn(1, 1, Sp, 128).to(torch.bfloat16)
+    refp = F.scaled_dot_product_attention(qp, kp, vp, is_causal=True, enable_gqa=True)[0]
+    same = tot = 0
+    for p in (0, 1, 77, 511, 512, 539):
+        for h in range(4):
+            got = attend_row(qp[0, h, p], kp[0, 0, : p + 1], vp[0, 0, : p + 1])
+            same += int((got == refp[h, p]).sum())
+            tot += 128
+    assert same / tot > 0.8

@@ -24,14 +24,13 @@ class GemvArgs(ctypes.Structure):
     _fields_ = [
         ("W", c_void_p), ("X", c_void_p),
         ("M", c_int), ("N", c_int), ("K", c_int), ("ldx", c_int),
-        ("ksplit", c_int), ("nchunk", c_int),
+        ("groups", c_int), ("reserved", c_int),
         ("ln_w", c_void_p), ("ln_b", c_void_p), ("eps", c_float),
         ("out", c_void_p), ("ldo", c_int), ("n_valid", c_int),
         ("row_kv", c_void_p), ("row_pos", c_void_p),
         ("k_cache", c_void_p), ("v_cache", c_void_p),
         ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
-        ("rope", c_void_p), ("slab", c_void_p), ("counters", c_void_p),
-        ("slab_cap", c_int64), ("counters_cap", c_int64),
+        ("rope", c_void_p),
     ]
 
 
@@ -51,25 +50,6 @@ class Slots(ctypes.Structure):
     ]
 
 
-class StepLayer(ctypes.Structure):
-    _fields_ = [
-        ("ln1_w", c_void_p), ("ln1_b", c_void_p), ("ln2_w", c_void_p), ("ln2_b", c_void_p),
-        ("qkv", c_void_p), ("out", c_void_p), ("fc1", c_void_p), ("fc2", c_void_p),
-        ("k_cache", c_void_p), ("v_cache", c_void_p),
-    ]
-
-
-class StepArgs(ctypes.Structure):
-    _fields_ = [
-        ("layers", c_void_p), ("tasks", c_void_p), ("task_hdr", c_void_p),
-        ("x", c_void_p), ("row_pos", c_void_p), ("rope", c_void_p),
-        ("heads", c_void_p), ("nf_w", c_void_p), ("nf_b", c_void_p), ("logits", c_void_p),
-        ("granules", c_void_p), ("ctl", c_void_p), ("stamps", c_void_p),
-        ("rows", c_int), ("n_layer", c_int), ("smax", c_int), ("n_blocks", c_int),
-        ("att_cus", c_int), ("att_pmax", c_int), ("eps", c_float), ("tokens", c_int),
-    ]
-
-
 class CondParam(ctypes.Structure):
     _fields_ = [("table", c_void_p), ("weight", c_void_p), ("bias", c_void_p), ("in_dim", c_int), ("pad", c_int),
                 ("min_val", c_float), ("max_val", c_float)]
@@ -85,16 +65,9 @@ COND_EMBED, COND_VECTOR, COND_FOURIER, COND_LINEAR, COND_PASSTHROUGH = range(5)
 _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
-    "zmi_gemv_slab_floats": (c_int64, [c_int, c_int, c_int, c_int]),
-    "zmi_layernorm_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
-                                   c_void_p]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
-    "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
-    "zmi_step_granule_words": (c_int64, [c_int, c_int, c_int]),
-    "zmi_step_lds_bytes": (c_int64, [c_int, c_int]),
-    "zmi_step_blocks": (c_int, [c_int, c_int]),
-    "zmi_step_launch": (c_int, [ctypes.POINTER(StepArgs), c_void_p]),
+                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -111,7 +84,6 @@ _SIGS = {
     "zmi_prefix_condition": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                      c_void_p, c_void_p]),
     "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),
-    "zmi_prefetch": (c_int, [c_void_p, c_int64, c_int, c_void_p]),
     "zmi_graph_begin": (c_int, [c_void_p]),
     "zmi_graph_end": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     "zmi_graph_launch": (c_int, [c_void_p, c_int, c_void_p]),

@@ -10,10 +10,9 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libzonos_hip.so")
-LIB_STAMPS = os.path.join(HERE, "libzonos_hip_stamps.so")
-SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + [ "zmi_attn.hip", "zmi_sample.hip", "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip",
-           "zmi_step.hip"]
-HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_gemv8_impl.h"]
+SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + ["zmi_attn.hip", "zmi_sample.hip",
+                                                                        "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip"]
+HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result",
          f"-I{INCLUDE}", f"-I{CSRC}"]
@@ -26,13 +25,10 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8, stamps: str | bool = False) -> str:
-    """stamps builds the diagnostic libzonos_hip_stamps.so with in-kernel timestamps: "step" (or True)
-    for the persistent step kernel (-DZMI_STEP_STAMPS, tools/step_stamps.py), "gemv" for the decode
-    GEMV of the launch path (-DZMI_STAMPS, tools/stamps.py; its stamps need a large split-K slab)."""
-    objdir = os.path.join(HERE, "build_stamps" if stamps else "build")
-    lib = LIB_STAMPS if stamps else LIB
-    flags = FLAGS + ({"gemv": ["-DZMI_STAMPS"]}.get(stamps, ["-DZMI_STEP_STAMPS"]) if stamps else [])
+def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
+    objdir = os.path.join(HERE, "build")
+    lib = LIB
+    flags = FLAGS
     os.makedirs(objdir, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "zonos_hip.h")]
     objs, procs = [], []
@@ -68,4 +64,4 @@ def _wait(item):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, stamps="gemv" if "--gemv-stamps" in sys.argv else "--stamps" in sys.argv)
+    build(force="--force" in sys.argv)

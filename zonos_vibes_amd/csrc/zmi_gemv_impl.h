@@ -1,202 +1,187 @@
-// GEMV kernel template + launch helpers, included by the per-epilogue translation units
-// (zmi_gemv_e*.hip) so the ~100 instantiations compile in parallel.
+// Weight-streaming GEMV / skinny GEMM for the decode step and the prefill, gfx950.
+//
+// out[m, n] = sum_k A[m, k] * W[n, k]   (nn.Linear, reference zonos/backbone/_torch.py:114-115,147-152,
+//                                        heads: zonos/model.py:100-101)
+//
+// One kernel for every row count M (decode: M = 2 x slots; prefill: M = 2 x prefill length), so a
+// row's result never depends on how many rows share the launch (batched output
+// must equal the reference's batch_size=1 output, model.py:194):
+//
+//  * a workgroup owns G groups of 8 output columns over the WHOLE K, and a tile of RT rows;
+//    W waves per group split K into fixed segments; every lane issues all of its weight loads
+//    (NL x 16 B, straight into VGPRs) before it needs the first one. Row tiles of one column
+//    block re-read the weights (from L2 when they run together: the block -> tile map below puts
+//    them on one XCD, consecutive in dispatch order; speed only, never correctness).
+//  * the products run on MFMA v_mfma_f32_16x16x32_bf16 with 8 real columns per 16-column tile:
+//    lane l of a 1 KiB weight chunk holds column 8g + (l & 7) at k = 64 kc + 32 ((l >> 3) & 1) +
+//    8 (l >> 4) .. +7 (layout "M8", zmi_pack_weight). Against the activation k-half 0 the
+//    tile's columns 0..7 are exact partial sums, against k-half 1 its columns 8..15 are; the
+//    other half of each tile is discarded. Each chunk therefore costs two MFMAs and no lane
+//    movement, and a tile carries up to 16 rows for the same cost as one.
+//  * fixed reduction order, independent of M and of the tile a row lands in: per wave a
+//    chain of MFMAs over its k-segment (k-half 0 and k-half 1 in two accumulators), their sum,
+//    then the W segment sums in wave order.
+//  * optional LayerNorm prologue (nn.LayerNorm, _torch.py:62,88,90): one wave per row, fp32
+//    two-pass statistics, bf16-rounded output, the same arithmetic for every row.
+//  * fused epilogues: bf16 store, residual add, RoPE + KV-cache write, SwiGLU, logits, raw f32.
 #pragma once
 #include "zmi_common.h"
 #include "zmi_kernels.h"
 
 namespace zmi_gemv {
 
-
 constexpr int PRO_PLAIN = 0, PRO_LN = 1;
-constexpr int XS_GLOBAL = 0, XS_REG = 1, XS_DMA = 2;  // where the A-operand rows come from
+constexpr size_t LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
-template <int MT>
-struct GemvLds {
-  static constexpr int RED = 0;
-  static constexpr int TILE = RED + 4 * MT * 64 * 4 * 4;
-  static constexpr int LN = TILE + MT * 16 * 17 * 4;
-  static constexpr int FLAG = LN + 2 * MT * 16 * 4;
-  static constexpr int XS = FLAG + 16;
+// DPP row_ror:8 — lane i of each 16-lane row reads lane (i + 8) & 15 of the same row
+__device__ __forceinline__ float ror8(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ void dma_piece(const bf16_t* gsrc, bf16_t* ldp) {
+  // one 1 KiB LDS-DMA piece (64 lanes x 16 B, lane-linear). Inline asm: the compiler does not
+  // count it, so the covering wait is the explicit vmcnt after the weight loads
+  // (cdna_hip_programming.md §5.7).
+  const unsigned ldst =
+      __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) void*)ldp);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(ldst)
+               : "memory");
+}
+
+// LDS image: rows of x at a stride of K + 8 bf16 (2K + 16 bytes: the 16 rows of an MFMA
+// A-fragment read fall on distinct 16-byte bank slots), gamma / beta, then the segment sums.
+template <int K>
+struct Img {
+  static constexpr int XROW = K + 8;
+  static size_t bytes(int rows, int nwv, int rt, bool ln) {
+    return (size_t)rows * XROW * 2 + (ln ? (size_t)4 * K : 0) + (size_t)nwv * 8 * rt * 4;
+  }
 };
 
-template <int MT, int NF, int PRO, int EPI, int XLDS>
-__global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
-  // all LDS in one dynamic block, carved at 16 B multiples (no static __shared__ shifting the base:
-  // cdna_hip_programming.md §6 Guideline 17)
+template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
+__global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt) {
+  constexpr int K = W * NL * 64;
+  constexpr int KC = K / 64;
+  constexpr int NWV = G * W;
+  constexpr int XROW = Img<K>::XROW;
+  static_assert(RT == 8 || RT == 16, "row tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float(&red)[4][MT][64][4] = *reinterpret_cast<float(*)[4][MT][64][4]>(smem);
-  float(&tile)[MT * 16][17] = *reinterpret_cast<float(*)[MT * 16][17]>(smem + GemvLds<MT>::TILE);
-  float* ln_mean = reinterpret_cast<float*>(smem + GemvLds<MT>::LN);
-  float* ln_rstd = ln_mean + MT * 16;
-  unsigned& last_flag = *reinterpret_cast<unsigned*>(smem + GemvLds<MT>::FLAG);
-  bf16_t* xs = reinterpret_cast<bf16_t*>(smem + GemvLds<MT>::XS);  // XLDS: activation rows [rows][ldx_s]
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NT = a.N >> 4, KT = a.K >> 5;
-  int b = blockIdx.x;
-  const int nb = gridDim.x;
-  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);  // XCD-contiguous tiles (speed only)
-  const int nt = b / a.ksplit, ks = b - nt * a.ksplit;
-  const int row0 = blockIdx.y * (MT * 16);
-  const int rows = min(MT * 16, a.M - row0);
-  const int kt_blk = KT / a.ksplit;
-  const int kt_base = ks * kt_blk;
-  const int kb0 = kt_base * 32, KB = kt_blk * 32;
+  // block -> (column block, row tile): the row tiles of one column block take ids 8 apart
+  const int b = blockIdx.x;
+  const int idx = b >> 3;
+  const int cb = (idx / n_rt) * 8 + (b & 7), rt = idx - (idx / n_rt) * n_rt;
+  if (cb >= n_cb) return;  // padding block: exits before any barrier
+  const int alloc_rows = a.M < RT ? a.M : RT;
+  const int row0 = rt * RT;
+  const int rows = min(RT, a.M - row0);
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* gam = xs + (size_t)alloc_rows * XROW;
+  bf16_t* bet = gam + K;
+  float* red = reinterpret_cast<float*>(smem + (size_t)alloc_rows * XROW * 2 + (PRO == PRO_LN ? 4 * K : 0));
 
-  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X);
-  const bf16_t* lnw = reinterpret_cast<const bf16_t*>(a.ln_w);
-  const bf16_t* lnb = reinterpret_cast<const bf16_t*>(a.ln_b);
-  // V8 weight layout (zmi_gemv8_impl.h): the MFMA B fragment (n = lane & 15, k = 8 (lane >> 4) of a
-  // 16 x 32 tile) of K-tile kt sits at  wlane + (kt >> 1) * 64 + (kt & 1) * 4  (uint4 units)
-  const int wn = nt * 16 + (lane & 15);
-  const u32x4_t* wlane = reinterpret_cast<const u32x4_t*>(a.W) + ((size_t)(wn >> 3) * (a.K >> 6)) * 64 +
-                         (wn & 7) * 8 + (lane >> 4);
-  auto wfrag = [&](int kt) { return __builtin_nontemporal_load(wlane + (size_t)(kt >> 1) * 64 + (kt & 1) * 4); };
-  const int arow = lane & 15, kq = (lane >> 4) * 8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR descriptors, no waterfalls
+  const int gi = wave / W, wk = wave - gi * W;
+  const int ngroups = a.N >> 3;
+  const int g_raw = cb * G + gi;
+  const bool g_ok = g_raw < ngroups;
+  const int g = g_ok ? g_raw : ngroups - 1;  // clamped: every wave joins the barriers
+  const int col0 = g * 8;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)row0 * a.ldx;
 
-  // (1) activation rows first (they gate the LayerNorm): up to 4 x 16 B per thread into registers,
-  //     unconditional loads from clamped addresses (no branch -> no vmcnt(0) per load)
-  const int xw = (PRO == PRO_LN) ? a.K : KB;          // columns staged per row
-  const int xk0 = (PRO == PRO_LN) ? 0 : kb0;          // first staged column
-  const int ldx_s = xw + 8;
-  const int per_row = xw >> 3, n_x = rows * per_row;
-  uint4 xr[4];
-  if (XLDS == XS_DMA) {
-    // 1 KiB LDS-DMA pieces (64 lanes x 16 B, lane-linear, never crossing a row): no VGPRs, so the
-    // weight stream below is not held back by register reuse
-    // Issued as inline asm: the compiler then does not treat the in-flight DMA as a pending LDS
-    // write and does not drain the whole vm queue (the weights) before the first ds_read; the
-    // covering wait is the explicit vmcnt(NF) below (cdna_hip_programming.md §5.7).
-    // pieces: activation rows, then (LayerNorm) gamma and beta of this block's k-range
-    const int ppr = xw >> 9, n_x_pc = rows * ppr, ppk = KB >> 9;
-    const int n_pc = n_x_pc + (PRO == PRO_LN ? 2 * ppk : 0);
-    for (int pc = wave; pc < n_pc; pc += 4) {
-      const bf16_t* gsrc;
-      bf16_t* ldp;
-      if (pc < n_x_pc) {
-        const int r = pc / ppr, p = pc - r * ppr;
-        gsrc = X + (size_t)(row0 + r) * a.ldx + xk0 + p * 512 + lane * 8;
-        ldp = xs + r * ldx_s + p * 512;
+  // (1) activation rows (+ LayerNorm gamma / beta) into LDS by DMA, 1 KiB pieces spread over waves
+  {
+    constexpr int PPR = K / 512;
+    const int n_x = rows * PPR;
+    const int n_pc = n_x + (PRO == PRO_LN ? 2 * PPR : 0);
+    for (int pc = wave; pc < n_pc; pc += NWV) {
+      if (pc < n_x) {
+        const int r = pc / PPR, p = pc - r * PPR;
+        dma_piece(X + (size_t)r * a.ldx + p * 512 + lane * 8, xs + r * XROW + p * 512);
       } else {
-        const int q = pc - n_x_pc, which = q / ppk, p = q - which * ppk;
-        gsrc = (which ? lnb : lnw) + kb0 + p * 512 + lane * 8;
-        ldp = xs + rows * ldx_s + which * KB + p * 512;
+        const int q = pc - n_x, which = q / PPR, p = q - which * PPR;
+        const bf16_t* src = reinterpret_cast<const bf16_t*>(which ? a.ln_b : a.ln_w);
+        dma_piece(src + p * 512 + lane * 8, (which ? bet : gam) + p * 512);
       }
-      const unsigned ldst = __builtin_amdgcn_readfirstlane(
-          (unsigned)(size_t)(__attribute__((address_space(3))) void*)ldp);
-      unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-                   "s_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(gsrc), "s"(ldst)
-                   : "memory");
-    }
-  } else if (XLDS == XS_REG) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int e = threadIdx.x + i * 256;
-      e = e < n_x ? e : n_x - 1;
-      const int r = e / per_row, c = (e - r * per_row) * 8;
-      xr[i] = *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + xk0 + c);
     }
   }
-  // epilogue operands needed only at the end, fetched now so their latency hides under the stream
-  // (decode-sized blocks: one (row, column pair) per thread)
-  const int col0 = nt * 16;
-  const bool pre = rows * 16 <= 256;
+  // epilogue operands that need no other load (older than the weights: covered by the vmcnt below).
+  // The group's first wave runs the epilogue; its lane handles outputs e = lane + 64 i.
+  const bool ew = (wk == 0) && g_ok;
+  constexpr int NE = (8 * RT + 63) / 64;
+  uint32_t res_pre[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) res_pre[i] = 0;
   int q_pos = -1, q_kvr = 0;
-  if (EPI == ZMI_EPI_QKV && pre && (int)threadIdx.x < rows * 8) {
-    q_pos = a.row_pos[row0 + (threadIdx.x >> 3)];
-    q_kvr = a.row_kv[row0 + (threadIdx.x >> 3)];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep the activation loads ahead of the weight stream
-  // (2) the weight stream does not depend on the activations: issue chunk 0 right away
-  u32x4_t wf[NF];
+  if (EPI == ZMI_EPI_RESIDUAL && ew) {
 #pragma unroll
-  for (int f = 0; f < NF; ++f) wf[f] = wfrag(kt_base + wave * NF + f);
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i, r = e >> 3, n = col0 + (e & 7);
+      if (r < rows && n < a.n_valid)
+        res_pre[i] = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + n];
+    }
+  }
+  if (EPI == ZMI_EPI_QKV && ew && (lane >> 2) < rows) {
+    q_pos = a.row_pos[row0 + (lane >> 2)];
+    q_kvr = a.row_kv[row0 + (lane >> 2)];
+  }
   __builtin_amdgcn_sched_barrier(0);
-  uint32_t res_pre = 0;
-  float2 rope_pre = {1.f, 0.f};
-  if (EPI == ZMI_EPI_RESIDUAL && pre && (int)threadIdx.x < rows * 16) {
-    const int n = col0 + (threadIdx.x & 15);
-    if (n < a.n_valid)
-      res_pre = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + (threadIdx.x >> 4)) * a.ldo + n];
-  }
-  if (EPI == ZMI_EPI_QKV && pre && q_pos >= 0) {
-    const int n = col0 + (threadIdx.x & 7) * 2;
-    if (n < (a.hq + a.hkv) * a.hd) {
-      const int d = (n < a.hq * a.hd ? n : n - a.hq * a.hd) % a.hd;
-      rope_pre = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
-    }
-  }
+  // (2) the whole weight slice of this lane, in flight at once: one buffer descriptor per wave
+  // (wave-uniform base), lane offset in the VGPR, chunk offset j KiB folded into the instruction
+  // (cdna_hip_programming.md T8). Non-temporal when each weight is read once (one row tile).
+  const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)g * KC + wk * NL) * 1024;
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wbase), (short)0, NL * 1024, 0x00020000);
+  u32x4_t wf[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, NTW ? 2 : 0);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // DMA pieces + epilogue operands landed
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
 
-  // (3) activations visible in LDS while the weights are still in flight; LayerNorm statistics
-  if (XLDS == XS_DMA) {
-    // this wave's DMA pieces are older than its NF weight loads; a raw barrier (no vmcnt(0) drain)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  } else if (XLDS == XS_REG) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = threadIdx.x + i * 256;
-      if (e < n_x) {
-        const int r = e / per_row, c = (e - r * per_row) * 8;
-        *reinterpret_cast<uint4*>(xs + r * ldx_s + c) = xr[i];
-      }
-    }
-    for (int e = threadIdx.x + 1024; e < n_x; e += 256) {
-      const int r = e / per_row, c = (e - r * per_row) * 8;
-      *reinterpret_cast<uint4*>(xs + r * ldx_s + c) =
-          *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + xk0 + c);
-    }
-    __syncthreads();
-  }
+  // (3) LayerNorm, one wave per row: lane owns the 8-element chunks lane + 64 i of the row; fp32
+  // sums in a fixed lane order, DPP wave reduction, bf16-rounded result written back in place.
   if (PRO == PRO_LN) {
-    for (int r = wave; r < rows; r += 4) {
+    constexpr int CPL = K / 512;
+    for (int r = wave; r < rows; r += NWV) {
+      bf16_t* xr = xs + r * XROW;
+      uint4 xv[CPL];
       float s = 0.f;
-      for (int k = lane * 8; k < a.K; k += 512) {
-        const uint4 v = XLDS ? *reinterpret_cast<const uint4*>(xs + r * ldx_s + k)
-                             : *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + k);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s += bf2f(u[j]) + bf2f(u[j] >> 16);
+      for (int i = 0; i < CPL; ++i) {
+        xv[i] = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
+        const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t += bf2f(u[j]) + bf2f(u[j] >> 16);
+        s += t;
       }
-      const float mean = wave_sum(s) / (float)a.K;
+      const float mean = wave_sum(s) / (float)K;
       float ss = 0.f;
-      for (int k = lane * 8; k < a.K; k += 512) {
-        const uint4 v = XLDS ? *reinterpret_cast<const uint4*>(xs + r * ldx_s + k)
-                             : *reinterpret_cast<const uint4*>(X + (size_t)(row0 + r) * a.ldx + k);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+        float t = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
-          ss += d0 * d0 + d1 * d1;
+          t += d0 * d0 + d1 * d1;
         }
+        ss += t;
       }
-      const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)a.K + a.eps);  // all lanes: wave reduction
-      if (lane == 0) {
-        ln_mean[r] = mean;
-        ln_rstd[r] = rstd;
-      }
-    }
-    __syncthreads();
-    if (XLDS) {  // normalise this block's k-range in place: (x * rstd + (-mean * rstd)) * gamma + beta
-      const int per_row = KB >> 3;
-      for (int e = threadIdx.x; e < rows * per_row; e += 256) {
-        const int r = e / per_row, c = kb0 + (e - r * per_row) * 8;
-        uint4* p = reinterpret_cast<uint4*>(xs + r * ldx_s + c);
-        uint4 gw, gb;
-        if (XLDS == XS_DMA) {  // gamma / beta were DMA'd next to the rows
-          gw = *reinterpret_cast<const uint4*>(xs + rows * ldx_s + (c - kb0));
-          gb = *reinterpret_cast<const uint4*>(xs + rows * ldx_s + KB + (c - kb0));
-        } else {
-          gw = *reinterpret_cast<const uint4*>(lnw + c);
-          gb = *reinterpret_cast<const uint4*>(lnb + c);
-        }
-        const uint4 v = *p;
-        const float rstd = ln_rstd[r], nbias = -ln_mean[r] * rstd;
-        uint32_t u[4] = {v.x, v.y, v.z, v.w};
+      const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)K + a.eps), nbias = -mean * rstd;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
+        const uint4 gb = *reinterpret_cast<const uint4*>(bet + c * 8);
+        uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
         const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -204,136 +189,86 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
           const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
           u[j] = f2bf(y0) | (f2bf(y1) << 16);
         }
-        *p = uint4{u[0], u[1], u[2], u[3]};
+        *reinterpret_cast<uint4*>(xr + c * 8) = uint4{u[0], u[1], u[2], u[3]};
       }
-      __syncthreads();
-    }
-  }
-
-  f32x4_t acc[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  for (int c = 0; c < a.nchunk; ++c) {
-    const int ktc = (c * 4 + wave) * NF;
-    if (c > 0) {
-#pragma unroll
-      for (int f = 0; f < NF; ++f) wf[f] = wfrag(kt_base + ktc + f);
-    }
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int k0 = (kt_base + ktc + f) * 32 + kq;  // absolute k of this lane's 8 elements
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int r = mt * 16 + arow;
-        const int rc = r < rows ? r : rows - 1;       // clamped: no branch around the load
-        const uint32_t keep = r < rows ? 0xffffffffu : 0u;
-        uint4 xv;
-        if (XLDS) {
-          xv = *reinterpret_cast<const uint4*>(xs + rc * ldx_s + (k0 - xk0));
-        } else {
-          xv = *reinterpret_cast<const uint4*>(X + (size_t)(row0 + rc) * a.ldx + k0);
-          if (PRO == PRO_LN) {
-            const uint4 lw = *reinterpret_cast<const uint4*>(lnw + k0);
-            const uint4 lb = *reinterpret_cast<const uint4*>(lnb + k0);
-            const float rstd = ln_rstd[rc], nbias = -ln_mean[rc] * rstd;
-            uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
-            const uint32_t uw[4] = {lw.x, lw.y, lw.z, lw.w}, ub[4] = {lb.x, lb.y, lb.z, lb.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float y0 = (bf2f(u[j]) * rstd + nbias) * bf2f(uw[j]) + bf2f(ub[j]);
-              const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
-              u[j] = f2bf(y0) | (f2bf(y1) << 16);
-            }
-            xv = uint4{u[0], u[1], u[2], u[3]};
-          }
-        }
-        xv.x &= keep;
-        xv.y &= keep;
-        xv.z &= keep;
-        xv.w &= keep;
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xv),
-                                                          __builtin_bit_cast(bf16x8_t, wf[f]), acc[mt], 0, 0, 0);
-      }
-    }
-  }
-
-  // ---- fixed-order cross-wave reduction -> tile[m][n] ----
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][mt][lane][r] = acc[mt][r];
-  __syncthreads();
-  for (int e = threadIdx.x; e < MT * 256; e += 256) {
-    const int mt = e >> 8, l = (e >> 2) & 63, r = e & 3;
-    const float v = ((red[0][mt][l][r] + red[1][mt][l][r]) + red[2][mt][l][r]) + red[3][mt][l][r];
-    tile[mt * 16 + (l >> 4) * 4 + r][l & 15] = v;
-  }
-  __syncthreads();
-
-  // ---- split-K: publish slab, last arriver sums slabs in ks order ----
-  if (a.ksplit > 1) {
-    const size_t tid = (size_t)blockIdx.y * NT + nt;
-    float* slab = a.slab + tid * (size_t)a.ksplit * (MT * 256);
-    for (int e = threadIdx.x; e < rows * 16; e += 256) st_wt(slab + (size_t)ks * (MT * 256) + e, tile[e >> 4][e & 15]);
-    if (!zmi_last_arriver_wt(a.counters + tid, (unsigned)a.ksplit, &last_flag)) return;
-    for (int e = threadIdx.x; e < rows * 16; e += 256) {
-      float v = ld_wt(slab + e);
-      for (int s = 1; s < a.ksplit; ++s) v += ld_wt(slab + (size_t)s * (MT * 256) + e);
-      tile[e >> 4][e & 15] = v;
     }
     __syncthreads();
   }
 
-  // ---- fused epilogues ----
-  if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32) {
-    for (int e = threadIdx.x; e < rows * 16; e += 256) {
-      const int m = e >> 4, n = col0 + (e & 15);
-      if (n >= a.n_valid) continue;
-      const float v = tile[m][e & 15];
-      const size_t o = (size_t)(row0 + m) * a.ldo + n;
+  // (4) MFMA chain over this wave's k-segment. A operand: lane l reads row l & 15 (rows past the
+  // tile re-read its last row; those outputs are discarded), k = 8 (l >> 4) .. +7 of the k-half.
+  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int ar = min(lane & 15, rows - 1);
+    const bf16_t* xa = xs + ar * XROW + wk * NL * 64 + (lane >> 4) * 8;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const uint4 x0 = *reinterpret_cast<const uint4*>(xa + j * 64);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(xa + j * 64 + 32);
+      const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[j]);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), wv, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), wv, acc1, 0, 0, 0);
+    }
+  }
+  // (5) segment sum = k-half 0 (tile columns 0..7) + k-half 1 (tile columns 8..15, moved down by
+  // DPP); accumulator element q of lane l is row 4 (l >> 4) + q, column l & 15
+  {
+    const int c = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = acc0[q] + ror8(acc1[q]);
+      if (c < 8 && rb + q < RT) red[(wave * 8 + c) * RT + rb + q] = v;
+    }
+  }
+  __syncthreads();
+  if (!ew) return;
+  auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
+    float v = red[((gi * W) * 8 + c) * RT + r];
+#pragma unroll
+    for (int w = 1; w < W; ++w) v += red[((gi * W + w) * 8 + c) * RT + r];
+    return v;
+  };
+
+  // (6) fused epilogues
+  if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
+      if (r >= rows || n >= a.n_valid) continue;
+      const float v = colsum(c, r);
+      const size_t m = (size_t)(row0 + r);
       if (EPI == ZMI_EPI_F32) {
-        reinterpret_cast<float*>(a.out)[o] = v;
+        reinterpret_cast<float*>(a.out)[m * a.ldo + n] = v;
       } else if (EPI == ZMI_EPI_STORE) {
-        reinterpret_cast<bf16_t*>(a.out)[o] = (bf16_t)f2bf(v);
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(v);
+      } else if (EPI == ZMI_EPI_RESIDUAL) {
+        // x + bf16(linear(x))  (_torch.py:100-101)
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(bf2f(res_pre[i]) + bfround(v));
       } else {
-        bf16_t* p = reinterpret_cast<bf16_t*>(a.out) + o;
-        const uint32_t xin = pre ? res_pre : (uint32_t)*p;  // prefetched when one element per thread
-        *p = (bf16_t)f2bf(bf2f(xin) + bfround(v));  // x + bf16(linear(x))  (_torch.py:100-101)
+        // 9 heads back to back, 1026 columns each (1025 real + the zero pad row)
+        const int cbk = n / 1026, vv = n - cbk * 1026;
+        reinterpret_cast<float*>(a.out)[(m * 9 + cbk) * 1026 + vv] = bfround(v);
       }
     }
-  } else if (EPI == ZMI_EPI_LOGITS) {
-    // 9 heads packed back to back, 1026 columns each (1025 real + the zero pad row)
-    for (int e = threadIdx.x; e < rows * 16; e += 256) {
-      const int m = e >> 4, n = col0 + (e & 15);
-      if (n >= a.n_valid) continue;
-      const int cb = n / 1026, v = n - cb * 1026;
-      reinterpret_cast<float*>(a.out)[((size_t)(row0 + m) * 9 + cb) * 1026 + v] = bfround(tile[m][e & 15]);
-    }
   } else if (EPI == ZMI_EPI_SWIGLU) {
-    // V8 SwiGLU packing: each 8-column group = 4 value rows then their 4 gate rows, so tile
-    // column 8h + c (c < 4) is value row 8nt + 4h + c and 8h + 4 + c its gate  (_torch.py:150-152)
-    for (int e = threadIdx.x; e < rows * 8; e += 256) {
-      const int m = e >> 3, c = e & 7, h = c >> 2, c4 = c & 3;
-      const float y = bfround(tile[m][h * 8 + c4]);
-      const float g = bfround(tile[m][h * 8 + 4 + c4]);
-      const float sg = bfround(g / (1.0f + expf(-g)));
-      reinterpret_cast<bf16_t*>(a.out)[(size_t)(row0 + m) * a.ldo + nt * 8 + c] = (bf16_t)f2bf(y * sg);
+    // M8 SwiGLU packing: columns 0..3 = value rows 4g.., 4..7 = gate rows F + 4g..  (_torch.py:150-152)
+    const int r = lane >> 2, c = lane & 3;
+    if (r < rows) {
+      const float y = bfround(colsum(c, r));
+      const float gt = bfround(colsum(c + 4, r));
+      const float sg = bfround(gt / (1.0f + expf(-gt)));
+      reinterpret_cast<bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + g * 4 + c] = (bf16_t)f2bf(y * sg);
     }
   } else if (EPI == ZMI_EPI_QKV) {
-    // q | k | v split, interleaved-pair RoPE in fp32 on q and k, then KV-cache write (_torch.py:18-49,117-126)
-    const int qcols = a.hq * a.hd, kcols = a.hkv * a.hd;
-    for (int e = threadIdx.x; e < rows * 8; e += 256) {
-      const int m = e >> 3, c = (e & 7) * 2;
-      const int row = row0 + m;
-      const int pos = pre ? q_pos : a.row_pos[row];
-      if (pos < 0) continue;
+    // q | k | v split, interleaved-pair RoPE in fp32 on q and k, KV-cache write (_torch.py:18-49,117-126)
+    const int r = lane >> 2, c = (lane & 3) * 2;
+    if (r < rows && q_pos >= 0) {
       const int n = col0 + c;
-      float x0 = bfround(tile[m][c]), x1 = bfround(tile[m][c + 1]);
+      const int qcols = a.hq * a.hd, kcols = a.hkv * a.hd;
+      float x0 = bfround(colsum(c, r)), x1 = bfround(colsum(c + 1, r));
       if (n < qcols + kcols) {
         const int d = (n < qcols ? n : n - qcols) % a.hd;
-        const float2 cs =
-            pre ? rope_pre : *reinterpret_cast<const float2*>(a.rope + ((size_t)pos * (a.hd >> 1) + (d >> 1)) * 2);
+        const float2 cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
         const float co = cs.x, si = cs.y;
         const float r0 = x0 * co - x1 * si;
         const float r1 = x1 * co + x0 * si;
@@ -342,62 +277,89 @@ __global__ __launch_bounds__(256) void gemv_kernel(const ZmiGemvArgs a) {
       }
       const uint32_t packed = f2bf(x0) | (f2bf(x1) << 16);
       if (n < qcols) {
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)row * a.ldo + n) = packed;
-      } else {
-        const bool is_k = n < qcols + kcols;
-        const int nn = is_k ? n - qcols : n - qcols - kcols;
-        const int kh = nn / a.hd, d = nn - kh * a.hd;
-        bf16_t* cache = reinterpret_cast<bf16_t*>(is_k ? a.k_cache : a.v_cache);
-        const size_t o = (((size_t)(pre ? q_kvr : a.row_kv[row]) * a.hkv + kh) * a.smax + pos) * a.hd + d;
-        *reinterpret_cast<uint32_t*>(cache + o) = packed;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)(row0 + r) * a.ldo + n) = packed;
+      } else if (n < qcols + kcols) {  // K cache [row][kv head][position][hd]
+        const int nn = n - qcols, kh = nn / a.hd, d = nn - kh * a.hd;
+        const size_t o = (((size_t)q_kvr * a.hkv + kh) * a.smax + q_pos) * a.hd + d;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.k_cache) + o) = packed;
+      } else {  // V cache, transposed: [row][kv head][hd][position] (zmi_attn.hip's P.V operand)
+        const int nn = n - qcols - kcols, kh = nn / a.hd, d = nn - kh * a.hd;
+        bf16_t* vt = reinterpret_cast<bf16_t*>(a.v_cache) + (((size_t)q_kvr * a.hkv + kh) * a.hd + d) * a.smax + q_pos;
+        vt[0] = (bf16_t)(packed & 0xffffu);
+        vt[a.smax] = (bf16_t)(packed >> 16);
       }
     }
   }
 }
 
-template <int MT, int NF, int PRO, int EPI>
-hipError_t launch_t(const ZmiGemvArgs& a, hipStream_t s) {
-  dim3 grid((a.N >> 4) * a.ksplit, (a.M + MT * 16 - 1) / (MT * 16));
-  // stage the activation rows in LDS when they fit (always for decode-sized M)
-  const int rows = a.M < MT * 16 ? a.M : MT * 16;
-  const int xw = PRO == PRO_LN ? a.K : a.K / a.ksplit;
-  const int kb = a.K / a.ksplit;
-  const size_t lds = (size_t)rows * (xw + 8) * sizeof(bf16_t);
-  const size_t lds_dma = lds + (PRO == PRO_LN ? 2 * (size_t)kb * sizeof(bf16_t) : 0);
-  if (lds_dma <= 64 * 1024 && xw % 512 == 0 && kb % 512 == 0)
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_DMA>), grid, dim3(256), GemvLds<MT>::XS + lds_dma, s, a);
-  else if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_REG>), grid, dim3(256), GemvLds<MT>::XS + lds, s, a);
-  else
-    hipLaunchKernelGGL((gemv_kernel<MT, NF, PRO, EPI, XS_GLOBAL>), grid, dim3(256), GemvLds<MT>::XS, s, a);
+// (W, NL, RT) from K: K = 64 W NL. The LayerNorm'd K = 2048 projections stream 16 chunks per lane
+// from 2 waves per group; without LayerNorm 4 x 8 (round-1 measurements of the same streaming
+// structure, tools/bench_graph.py). K = 8192 holds 8 rows per tile (8 x 16 KiB of LDS).
+struct Shape {
+  int W, NL, RT;
+};
+inline bool shape_for(int K, bool ln, Shape* s) {
+  switch (K) {
+    case 512: *s = {2, 4, 16}; return true;
+    case 1024: *s = {4, 4, 16}; return true;
+    case 2048: *s = ln ? Shape{2, 16, 16} : Shape{4, 8, 16}; return true;
+    case 4096: *s = {4, 16, 16}; return true;
+    case 8192: *s = {8, 16, 8}; return true;
+  }
+  return false;
+}
+
+// column groups per block: 2 for the many-group LayerNorm'd projections (qkv, fc1, heads: the
+// block's LayerNorm and activation staging are then shared by 16 columns); `groups` > 0 overrides
+inline int groups_for(const ZmiGemvArgs& a, const Shape& s) {
+  if (a.groups > 0) return a.groups;
+  return (s.W == 2 && s.NL == 16 && a.N / 8 >= 384) ? 2 : 1;
+}
+
+template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
+hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
+  constexpr int K = W * NL * 64;
+  auto fn = gemv_kernel<G, W, NL, RT, PRO, EPI, NTW>;
+  const int n_cb = (a.N / 8 + G - 1) / G;
+  const int n_rt = (a.M + RT - 1) / RT;
+  const size_t lds = Img<K>::bytes(a.M < RT ? a.M : RT, G * W, RT, PRO == PRO_LN);
+  if (lds > LDS_MAX) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    static const hipError_t attr =  // once per instantiation: allow > 64 KiB of dynamic LDS
+        hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)LDS_MAX);
+    if (attr != hipSuccess) return attr;
+  }
+  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * n_rt;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt);
   return hipGetLastError();
 }
 
-template <int MT, int NF, int EPI>
-hipError_t launch_pro(const ZmiGemvArgs& a, hipStream_t s) {
-  return a.ln_w ? launch_t<MT, NF, PRO_LN, EPI>(a, s) : launch_t<MT, NF, PRO_PLAIN, EPI>(a, s);
-}
-
-template <int MT, int EPI>
-hipError_t launch_nf(const ZmiGemvArgs& a, int nf, hipStream_t s) {
-  switch (nf) {
-    case 2: return launch_pro<MT, 2, EPI>(a, s);
-    case 4: return launch_pro<MT, 4, EPI>(a, s);
-    case 8: return launch_pro<MT, 8, EPI>(a, s);
-    case 16: return launch_pro<MT, 16, EPI>(a, s);
-  }
-  return hipErrorInvalidValue;
+template <int G, int W, int NL, int RT, int EPI>
+hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
+  const bool ln = a.ln_w != nullptr;
+  const bool once = a.M <= RT;  // each weight read once: non-temporal loads
+  if (ln) return once ? launch_p<G, W, NL, RT, PRO_LN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_LN, EPI, 0>(a, s);
+  return once ? launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 0>(a, s);
 }
 
 template <int EPI>
-hipError_t launch_mt(const ZmiGemvArgs& a, int mt, int nf, hipStream_t s) {
-  switch (mt) {
-    case 1: return launch_nf<1, EPI>(a, nf, s);
-    case 2: return launch_nf<2, EPI>(a, nf, s);
-    case 4: return launch_nf<4, EPI>(a, nf, s);
-    case 8: return launch_nf<8, EPI>(a, nf, s);
-  }
-  return hipErrorInvalidValue;
+hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
+  Shape sh;
+  if (!shape_for(a.K, a.ln_w != nullptr, &sh)) return hipErrorInvalidValue;
+  const int g = groups_for(a, sh);
+#define ZMI_SHAPE(G_, W_, NL_, RT_) \
+  if (g == G_ && sh.W == W_ && sh.NL == NL_ && sh.RT == RT_) return launch_g<G_, W_, NL_, RT_, EPI>(a, s);
+  ZMI_SHAPE(1, 2, 4, 16)
+  ZMI_SHAPE(1, 4, 4, 16)
+  ZMI_SHAPE(1, 2, 16, 16)
+  ZMI_SHAPE(2, 2, 16, 16)
+  ZMI_SHAPE(1, 4, 8, 16)
+  ZMI_SHAPE(1, 4, 16, 16)
+  ZMI_SHAPE(1, 8, 16, 8)
+#undef ZMI_SHAPE
+  return hipErrorInvalidValue;  // e.g. groups = 2 outside the LayerNorm'd K = 2048 shape
 }
 
 }  // namespace zmi_gemv

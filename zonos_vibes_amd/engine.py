@@ -21,14 +21,11 @@ import numpy as np
 import torch
 
 from . import _lib
-from . import step_plan
 from . import synthetic as syn
 from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN, ZonosConfig
 
 HEADS_N = N_CODEBOOKS * 1026            # 9 heads x (1025 + 1 pad row), model.py:37 + utils.py:12-27
 HEADS_N_PAD = (HEADS_N + 15) // 16 * 16
-GEMV_COUNTERS = 1 << 16
-STEP_DIMS = (2048, 16, 4, 128, 8192)   # (d, heads, kv heads, head dim, ffn) the step kernel is built for
 
 
 def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
@@ -75,7 +72,7 @@ def _round8(n: int) -> int:
 
 class HipEngine:
     def __init__(self, cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
-                 max_prefill: int = 512, step_kernel: bool | None = None):
+                 max_prefill: int = 512):
         bb = cfg.backbone
         if bb.ssm_cfg:
             raise NotImplementedError("hybrid (mamba-ssm) backbone is not built (SURVEY.md §8f next #1)")
@@ -96,9 +93,9 @@ class HipEngine:
         self.stream = torch.cuda.Stream(self.dev)
         self.sptr = self.stream.cuda_stream
         self.w = None
-        self._graph = None
+        self._plans: dict[int, list] = {}
+        self._graphs: dict[int, int] = {}
         self._alloc()
-        self._setup_step(step_kernel)
 
     # ------------------------------------------------------------------ allocation
     def _alloc(self):
@@ -111,17 +108,13 @@ class HipEngine:
             self.logits = z(R, N_CODEBOOKS, 1026, dt=torch.float32)
             self.row_kv = z(R, dt=torch.int32)
             self.row_pos = torch.full((R,), -1, dtype=torch.int32, device=dev)  # every row inactive
-            self.kc = z(self.L, R, self.Hkv, self.smax, self.hd)
-            self.vc = z(self.L, R, self.Hkv, self.smax, self.hd)
-            slab = 0
-            for n, k in self._gemv_shapes():
-                slab = max(slab, self.lib.zmi_gemv_slab_floats(R, n, k, 0))
-            self.slab = z(max(slab, 1), dt=torch.float32)
-            self.gemv_cnt = z(GEMV_COUNTERS, dt=torch.int32)
+            self.kc = z(self.L, R, self.Hkv, self.smax, self.hd)   # K  [layer][row][kv head][position][hd]
+            self.vc = z(self.L, R, self.Hkv, self.hd, self.smax)   # V^T [layer][row][kv head][hd][position]
             nq = max(R, 2 * self.max_prefill)
-            self.attn_part = z(self.lib.zmi_attention_partial_floats(nq, self.H, self.Hkv, self.hd, self.smax - 1),
-                               dt=torch.float32)
-            self.attn_cnt = z(nq * self.Hkv, dt=torch.int32)
+            wb = self.lib.zmi_attention_work_bytes(nq, self.H, self.Hkv, self.hd, self.smax - 1)
+            if wb < 0:
+                raise ValueError("attention geometry not supported by the HIP kernel")
+            self.attn_work = z(wb, dt=torch.uint8)  # first word: hand-off timeout flag
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -130,7 +123,6 @@ class HipEngine:
             self.params = z(S * ctypes.sizeof(_lib.Sampling), dt=torch.uint8)
             P = self.max_prefill
             self.x_pre, self.q_pre, self.attn_pre = z(2 * P, d), z(2 * P, qd), z(2 * P, qd)
-            self.xn_pre = z(2 * P, d)  # LayerNorm'd prefill rows (zmi_layernorm_rows)
             self.h_pre = z(2 * P, self.F)
             self.row_kv_pre = z(2 * P, dt=torch.int32)
             self.row_pos_pre = z(2 * P, dt=torch.int32)
@@ -142,83 +134,6 @@ class HipEngine:
                                 self.delayed.data_ptr(), self.params.data_ptr(), self.st["total_len"].data_ptr(),
                                 self.tcap, S)
         self.stream.synchronize()
-
-    def _setup_step(self, want: bool | None):
-        """Persistent decode-step kernel (csrc/zmi_step.hip, plan: step_plan.py) for a one-slot engine
-        at Zonos-v0.1 dims, when asked for (step_kernel=True or ZMI_STEP=1); otherwise the per-op
-        launches captured in a hipGraph. The launch path is the default: measured at C2 (p = 591) it
-        takes 1.15 ms per step against 1.87 ms for the step kernel, whose grid-wide hand-offs cost
-        more than the launch boundaries they remove.
-        want=True makes an unavailable step kernel an error instead of a silent choice."""
-        self.step_cfg = None
-        self.step_args = None
-        if want is False or (want is None and os.environ.get("ZMI_STEP", "0") != "1"):
-            return
-        why = None
-        if (self.d, self.H, self.Hkv, self.hd, self.F) != STEP_DIMS:
-            why = f"dims {(self.d, self.H, self.Hkv, self.hd, self.F)} != {STEP_DIMS}"
-        elif self.R != 2:
-            why = f"{self.R} rows (the step kernel runs one CFG slot pair)"
-        else:
-            units = self.R * step_plan.HKV
-            cus = self.lib.zmi_step_blocks(self.R, 1)
-            att = cus // units if cus else 0
-            pmax = -(-self.smax // att) if att else 0
-            if att not in (8, 16, 32, 64) or att * units != cus:
-                why = f"{cus} CUs do not split into {units} attention units of 8/16/32/64"
-            elif self.lib.zmi_step_blocks(self.R, pmax) != cus:
-                why = f"{self.smax} KV positions exceed the step kernel's LDS"
-        if why is not None:
-            if want:
-                raise ValueError(f"step kernel unavailable: {why}")
-            return
-        plan = step_plan.build(cus, self.R)
-        with torch.cuda.stream(self.stream):
-            self.step_tasks = torch.from_numpy(plan.tasks.view(np.int32).copy()).to(self.dev)
-            self.step_hdr = torch.from_numpy(plan.hdr.reshape(-1).copy()).to(self.dev)
-            self.step_gran = torch.zeros(self.lib.zmi_step_granule_words(self.R, cus, self.L), dtype=torch.int64,
-                                         device=self.dev)
-            self.step_ctl = torch.tensor([1, 0, 0, 0], dtype=torch.int32).to(self.dev)  # epoch starts at 1
-        self.stream.synchronize()
-        self.step_cfg = dict(plan=plan, blocks=cus, att_cus=att, att_pmax=pmax)
-
-    def _build_step_args(self):
-        w = self.w
-        lt = (_lib.StepLayer * self.L)()
-        for i, lw in enumerate(w["layers"]):
-            lt[i] = _lib.StepLayer(lw["ln1_w"].data_ptr(), lw["ln1_b"].data_ptr(), lw["ln2_w"].data_ptr(),
-                                   lw["ln2_b"].data_ptr(), lw["qkv"].data_ptr(), lw["out"].data_ptr(),
-                                   lw["fc1"].data_ptr(), lw["fc2"].data_ptr(), self.kc[i].data_ptr(),
-                                   self.vc[i].data_ptr())
-        with torch.cuda.stream(self.stream):
-            self.step_layers = torch.frombuffer(bytearray(lt), dtype=torch.uint8).to(self.dev)
-        self.stream.synchronize()
-        a = _lib.StepArgs()
-        a.layers, a.tasks, a.task_hdr = self.step_layers.data_ptr(), self.step_tasks.data_ptr(), self.step_hdr.data_ptr()
-        a.x, a.row_pos, a.rope = self.x.data_ptr(), self.row_pos.data_ptr(), self.rope.data_ptr()
-        a.heads, a.nf_w, a.nf_b = w["heads"].data_ptr(), w["nf_w"].data_ptr(), w["nf_b"].data_ptr()
-        a.logits, a.granules, a.ctl = self.logits.data_ptr(), self.step_gran.data_ptr(), self.step_ctl.data_ptr()
-        a.rows, a.n_layer, a.smax = self.R, self.L, self.smax
-        a.n_blocks, a.att_cus, a.att_pmax = self.step_cfg["blocks"], self.step_cfg["att_cus"], self.step_cfg["att_pmax"]
-        a.eps = self.eps
-        a.tokens = int(os.environ.get("ZMI_STEP_TOKENS", "0"))  # tuning knob; 0 = library default
-        if os.environ.get("ZMI_STEP_STAMPS"):  # diagnostic build only (tools/step_stamps.py)
-            self.step_stamps = torch.zeros(self.step_cfg["blocks"] * (self.L + 1) * 16 + 8 * 16 * 128 * 8,
-                                           dtype=torch.int64, device=self.dev)
-            a.stamps = self.step_stamps.data_ptr()
-        self.step_args = a
-
-    def check_step(self):
-        """Raise if the step kernel gave up waiting on a hand-off (its bounded spins set ctl[2])."""
-        if self.step_args is not None:
-            err = int(self.step_ctl[2].item())
-            if err:
-                raise RuntimeError(f"decode-step kernel timed out waiting on a hand-off (code {err:#x})")
-
-    def _gemv_shapes(self):
-        qkv = (self.H + 2 * self.Hkv) * self.hd
-        return [(qkv, self.d), (self.d, self.H * self.hd), (2 * self.F, self.d), (self.d, self.F),
-                (HEADS_N_PAD, self.d)]
 
     # ------------------------------------------------------------------ weights
     def _pack(self, w: torch.Tensor, n_pad: int, mode: int = _lib.PACK_IDENTITY) -> torch.Tensor:
@@ -273,11 +188,9 @@ class HipEngine:
         self.load_state_dict(sd)
 
     # ------------------------------------------------------------------ launch plan
-    def _gemv(self, W, X, M, N, K, epi, out, ldo, n_valid=None, ln=None, kv=None, ksplit=0, row_kv=None,
-              row_pos=None):
+    def _gemv(self, W, X, M, N, K, epi, out, ldo, n_valid=None, ln=None, kv=None, row_kv=None, row_pos=None):
         a = _lib.GemvArgs()
         a.W, a.X, a.M, a.N, a.K, a.ldx = W.data_ptr(), X.data_ptr(), M, N, K, K
-        a.ksplit = ksplit
         if ln is not None:
             a.ln_w, a.ln_b = ln[0].data_ptr(), ln[1].data_ptr()
         a.eps = self.eps
@@ -288,8 +201,6 @@ class HipEngine:
             a.k_cache, a.v_cache = kv[0].data_ptr(), kv[1].data_ptr()
             a.smax, a.hq, a.hkv, a.hd = self.smax, self.H, self.Hkv, self.hd
             a.rope = self.rope.data_ptr()
-        a.slab, a.counters = self.slab.data_ptr(), self.gemv_cnt.data_ptr()
-        a.slab_cap, a.counters_cap = self.slab.numel(), self.gemv_cnt.numel()
         return (a, epi)
 
     def _run_gemv(self, item):
@@ -297,34 +208,44 @@ class HipEngine:
         _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
 
     def _build_plan(self):
-        """Pre-build the decode-step argument blocks (M = all 2*S rows)."""
-        w, R, d, qd = self.w, self.R, self.d, self.H * self.hd
-        qkv_n = (self.H + 2 * self.Hkv) * self.hd
-        plan = []
-        for i, lw in enumerate(w["layers"]):
-            kv = (self.kc[i], self.vc[i])
-            plan.append(("gemv", self._gemv(lw["qkv"], self.x, R, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                            ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv,
-                                            row_pos=self.row_pos)))
-            plan.append(("attn", i))
-            plan.append(("gemv", self._gemv(lw["out"], self.attn, R, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
-            plan.append(("gemv", self._gemv(lw["fc1"], self.x, R, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
-                                            ln=(lw["ln2_w"], lw["ln2_b"]))))
-            plan.append(("gemv", self._gemv(lw["fc2"], self.h, R, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
-        self._heads = self._gemv(w["heads"], self.x, R, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
-                                 n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))
-        self.plan = plan
-        if self.step_cfg is not None:
-            self._build_step_args()
-        if self._graph is not None:
-            _lib.check(self.lib.zmi_graph_destroy(self._graph))
-            self._graph = None
+        """Invalidate the per-row-count decode plans and graphs (new weights or buffers)."""
+        for g in self._graphs.values():
+            _lib.check(self.lib.zmi_graph_destroy(g))
+        self._graphs.clear()
+        self._plans.clear()
+
+    def _plan(self, rows: int) -> list:
+        """Decode-step launches for the first `rows` rows (slots 0 .. rows/2 - 1). Every kernel's
+        per-row arithmetic is independent of `rows`, so a slot decodes identically in any plan."""
+        if rows not in self._plans:
+            w, d, qd = self.w, self.d, self.H * self.hd
+            qkv_n = (self.H + 2 * self.Hkv) * self.hd
+            plan = []
+            for i, lw in enumerate(w["layers"]):
+                kv = (self.kc[i], self.vc[i])
+                plan.append(("gemv", self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                                ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv,
+                                                row_pos=self.row_pos)))
+                plan.append(("attn", i))
+                plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
+                plan.append(("gemv", self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
+                                                self.F, ln=(lw["ln2_w"], lw["ln2_b"]))))
+                plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
+            plan.append(("gemv", self._gemv(w["heads"], self.x, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
+                                            n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))))
+            self._plans[rows] = plan
+        return self._plans[rows]
 
     def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
         _lib.check(self.lib.zmi_attention(q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(),
                                           _lib.ptr(row_kv), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
                                           self.smax, max_pos, out.data_ptr(), self.H * self.hd,
-                                          self.attn_part.data_ptr(), self.attn_cnt.data_ptr(), self.sptr), "attention")
+                                          self.attn_work.data_ptr(), self.sptr), "attention")
+
+    def check_errors(self):
+        """Raise if an attention launch gave up waiting on a cross-block hand-off (bounded spin)."""
+        if int(self.attn_work[:4].view(torch.int32).item()):
+            raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
 
     def refresh_inputs(self):
         """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
@@ -340,42 +261,45 @@ class HipEngine:
                                             self.w["emb"].data_ptr(), self.d, self.x.data_ptr(),
                                             self.row_kv.data_ptr(), self.row_pos.data_ptr(), self.sptr), "sample")
 
-    def enqueue_step(self, noise: torch.Tensor | None = None):
-        """One decode step for every slot (reference model.py:276-307), enqueued on self.stream.
+    def _rows(self, slots: int | None) -> int:
+        s = self.S if slots is None else int(slots)
+        if not 1 <= s <= self.S:
+            raise ValueError(f"slots {s} outside 1..{self.S}")
+        return 2 * s
 
-        The step's input embeddings and (kv row, position) tables were written by the previous
-        sampler launch (or the prefill's), fused into its frame-write epilogue."""
-        if self.step_args is not None:
-            _lib.check(self.lib.zmi_step_launch(ctypes.byref(self.step_args), self.sptr), "step")
-        else:
-            for kind, item in self.plan:
-                if kind == "gemv":
-                    self._run_gemv(item)
-                else:
-                    # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
-                    self._attention(item, self.q, self.R, None, self.row_pos, self.smax - 1, self.attn)
-            self._run_gemv(self._heads)
-        self._sample(self.logits, noise, 0, 0, self.S)
+    def enqueue_step(self, noise: torch.Tensor | None = None, slots: int | None = None):
+        """One decode step for slots 0 .. slots-1 (default: all; reference model.py:276-307), enqueued
+        on self.stream. The step's input embeddings and (kv row, position) tables were written by
+        the previous sampler launch (or the prefill's), fused into its frame-write epilogue."""
+        rows = self._rows(slots)
+        for kind, item in self._plan(rows):
+            if kind == "gemv":
+                self._run_gemv(item)
+            else:
+                # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
+                self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
+        self._sample(self.logits, noise, 0, 0, rows // 2)
 
-    def capture(self):
-        if self._graph is None:
+    def capture(self, slots: int | None = None):
+        rows = self._rows(slots)
+        if rows not in self._graphs:
             _lib.check(self.lib.zmi_graph_begin(self.sptr), "graph_begin")
             try:
-                self.enqueue_step()
+                self.enqueue_step(slots=rows // 2)
             finally:
                 g = ctypes.c_void_p()
                 _lib.check(self.lib.zmi_graph_end(self.sptr, ctypes.byref(g)), "graph_end")
-            self._graph = g.value
-        return self._graph
+            self._graphs[rows] = g.value
+        return self._graphs[rows]
 
-    def step(self, n: int = 1, use_graph: bool = True):
+    def step(self, n: int = 1, use_graph: bool = True, slots: int | None = None):
         if n <= 0:
             return
         if use_graph:
-            _lib.check(self.lib.zmi_graph_launch(self.capture(), n, self.sptr), "graph_launch")
+            _lib.check(self.lib.zmi_graph_launch(self.capture(slots), n, self.sptr), "graph_launch")
         else:
             for _ in range(n):
-                self.enqueue_step()
+                self.enqueue_step(slots=slots)
 
     # ------------------------------------------------------------------ prefill
     def prefill(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
@@ -427,27 +351,24 @@ class HipEngine:
         return s_len
 
     def _prefill_layers(self, m: int, max_pos: int):
+        """The m = 2 x S prefill rows through every layer, with the decode step's kernels (same per-row
+        arithmetic; LayerNorm fused as the GEMV prologue)."""
         d, qd = self.d, self.H * self.hd
         qkv_n = (self.H + 2 * self.Hkv) * self.hd
-        def ln(wb):  # normalise the m prefill rows once; the GEMMs below take them plain
-            _lib.check(self.lib.zmi_layernorm_rows(self.x_pre.data_ptr(), d, m, d, wb[0].data_ptr(), wb[1].data_ptr(),
-                                                   self.eps, self.xn_pre.data_ptr(), d, self.sptr), "layernorm")
-            return self.xn_pre
-
         for i, lw in enumerate(self.w["layers"]):
-            self._run_gemv(self._gemv(lw["qkv"], ln((lw["ln1_w"], lw["ln1_b"])), m, qkv_n, d, _lib.EPI_QKV,
-                                      self.q_pre, qd, kv=(self.kc[i], self.vc[i]),
-                                      row_kv=self.row_kv_pre, row_pos=self.row_pos_pre, ksplit=1))
+            self._run_gemv(self._gemv(lw["qkv"], self.x_pre, m, qkv_n, d, _lib.EPI_QKV, self.q_pre, qd,
+                                      ln=(lw["ln1_w"], lw["ln1_b"]), kv=(self.kc[i], self.vc[i]),
+                                      row_kv=self.row_kv_pre, row_pos=self.row_pos_pre))
             self._attention(i, self.q_pre, m, self.row_kv_pre, self.row_pos_pre, max_pos, self.attn_pre)
-            self._run_gemv(self._gemv(lw["out"], self.attn_pre, m, d, qd, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
-            self._run_gemv(self._gemv(lw["fc1"], ln((lw["ln2_w"], lw["ln2_b"])), m, 2 * self.F, d, _lib.EPI_SWIGLU,
-                                      self.h_pre, self.F, ksplit=1))
-            self._run_gemv(self._gemv(lw["fc2"], self.h_pre, m, d, self.F, _lib.EPI_RESIDUAL, self.x_pre, d, ksplit=1))
+            self._run_gemv(self._gemv(lw["out"], self.attn_pre, m, d, qd, _lib.EPI_RESIDUAL, self.x_pre, d))
+            self._run_gemv(self._gemv(lw["fc1"], self.x_pre, m, 2 * self.F, d, _lib.EPI_SWIGLU, self.h_pre, self.F,
+                                      ln=(lw["ln2_w"], lw["ln2_b"])))
+            self._run_gemv(self._gemv(lw["fc2"], self.h_pre, m, d, self.F, _lib.EPI_RESIDUAL, self.x_pre, d))
 
     # ------------------------------------------------------------------ readback
     def slot_state(self, slot: int) -> dict:
         self.stream.synchronize()
-        self.check_step()
+        self.check_errors()
         return {k: int(v[slot].item()) for k, v in self.st.items()}
 
     def read_codes(self, slot: int) -> torch.Tensor:

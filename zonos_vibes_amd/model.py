@@ -30,14 +30,12 @@ def _draw_seed() -> int:
 
 class Zonos:
     def __init__(self, config: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
-                 max_prefill: int = 512, autoencoder: DACAutoencoder | None = None,
-                 step_kernel: bool | None = None):
+                 max_prefill: int = 512, autoencoder: DACAutoencoder | None = None):
         self.config = config
         self.eos_token_id = config.eos_token_id
         self.masked_token_id = config.masked_token_id
         self._device = torch.device(device)
-        self.step_kernel = step_kernel
-        self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill, step_kernel)
+        self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill)
         self.autoencoder = autoencoder if autoencoder is not None else DACAutoencoder(device)
         pcc = config.prefix_conditioner
         self.prefix_conditioner = (PrefixConditioner(pcc.conditioners, config.backbone.d_model, device, pcc.projection)
@@ -84,7 +82,7 @@ class Zonos:
         if slots > e.S or seqlen > e.smax or prefill > e.max_prefill:
             w = e.w
             self.engine = HipEngine(self.config, self._device, max(slots, e.S), max(seqlen, e.smax),
-                                    max(prefill, e.max_prefill), self.step_kernel)
+                                    max(prefill, e.max_prefill))
             self.engine.w = w
             self.engine._build_plan()
 
@@ -125,7 +123,7 @@ class Zonos:
         if callback is None:
             while step < max_steps:
                 n = min(chunk, max_steps - step)
-                e.step(n)
+                e.step(n, slots=1)
                 step += n
                 if bar is not None:
                     bar.update(n)
@@ -134,7 +132,7 @@ class Zonos:
         else:
             # exact reference semantics: the callback sees every frame and may stop the loop
             while step < max_steps:
-                e.step(1)
+                e.step(1, slots=1)
                 step += 1
                 if bar is not None:
                     bar.update(1)
@@ -161,18 +159,18 @@ class Zonos:
         seeds = list(seeds) if seeds is not None else [_draw_seed() for _ in range(n)]
         need_seq = max(c.shape[1] + (0 if p is None else p.shape[2]) + m + 9 for c, p, m in zip(conds, prefixes, mnt))
         need_pre = max(c.shape[1] + (0 if p is None else p.shape[2]) + 1 for c, p in zip(conds, prefixes))
-        slots = max_slots or n
-        self._ensure_capacity(min(slots, n), need_seq, need_pre)
+        slots = min(max_slots or n, n)
+        self._ensure_capacity(slots, need_seq, need_pre)
         e = self.engine
         # longest-processing-time first, so the tail is short
         order = sorted(range(n), key=lambda i: -mnt[i])
         queue = list(order)
-        owner = [-1] * e.S
+        owner = [-1] * slots
         results: list[torch.Tensor | None] = [None] * n
-        remaining = [0] * e.S
+        remaining = [0] * slots
 
         def fill():
-            for s in range(e.S):
+            for s in range(slots):
                 if owner[s] < 0 and queue:
                     i = queue.pop(0)
                     params = SamplingParams.from_dict(dict(sampling_params), cfg_scale, seeds[i])
@@ -183,10 +181,11 @@ class Zonos:
         fill()
         while any(o >= 0 for o in owner):
             k = min(chunk, max(r for s, r in enumerate(remaining) if owner[s] >= 0))
-            e.step(k)
+            e.step(k, slots=slots)
             e.stream.synchronize()
+            e.check_errors()
             act = e.st["active"].cpu()
-            for s in range(e.S):
+            for s in range(slots):
                 if owner[s] >= 0:
                     remaining[s] -= k
                     if not act[s]:
