@@ -64,14 +64,19 @@ int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
  * at zonos/backbone/_torch.py:136 for decode (1 query) and prefill (causal = position bound).
  * ------------------------------------------------------------------------------------- */
 /* K cache [rows][hkv][smax][hd], V cache transposed [rows][hkv][hd][smax] (bf16, as the QKV
- * epilogue writes them). q_kv_row may be NULL: query i then reads KV-cache row i (decode). Softmax in the
- * 512-key block structure of the reference's CPU kernel (probabilities rounded to bf16 before P.V).
- * `work` holds zmi_attention_work_bytes(n_query, hq, hkv, hd, max_pos) zero-initialised bytes,
- * re-armed by every launch; its first 4 bytes become nonzero if a cross-block hand-off timed out. */
+ * epilogue writes them). q_kv_row may be NULL: query i then reads KV-cache row i (decode).
+ * Softmax in the 512-key block structure of the reference's CPU kernel (probabilities rounded to
+ * bf16 before P.V). Keys are processed in chunks of zmi_attention_chunk() keys whose partials go
+ * to part_o [n_query*hkv][chunks][hq/hkv][hd] and part_lm [..][2] (zmi_attention_partial_floats
+ * floats of o; 1/64 of that for lm), merged in-kernel by each query's last-arriving chunk.
+ * `work` holds zmi_attention_work_bytes(...) zero-initialised bytes, re-armed by every launch; its
+ * first 4 bytes become nonzero if a cross-chunk hand-off timed out. */
 int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                   const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
-                  int ldo, void* work, void* stream);
+                  int ldo, float* part_o, float* part_lm, void* work, void* stream);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
+int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
+int zmi_attention_chunk(void);
 
 /* ---------------------------------------------------------------------------------------
  * Sampler + EOS state machine + delay-pattern frame write, per utterance slot.

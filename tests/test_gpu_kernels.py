@@ -165,12 +165,15 @@ def _attention(q, kc, vc, positions, kv_rows=None, hq=16, hkv=4):
     rp = torch.tensor(positions, dtype=torch.int32, device=DEV)
     rk = None if kv_rows is None else torch.tensor(kv_rows, dtype=torch.int32, device=DEV)
     work = torch.zeros(L.lib().zmi_attention_work_bytes(n, hq, hkv, hd, smax - 1), dtype=torch.uint8, device=DEV)
+    nf = L.lib().zmi_attention_partial_floats(n, hq, hkv, hd, smax - 1)
+    po = torch.zeros(nf, dtype=torch.float32, device=DEV)
+    plm = torch.zeros(nf // hd * 2, dtype=torch.float32, device=DEV)
     for _ in range(2):  # the second launch checks that the hand-off state re-armed itself
         L.check(L.lib().zmi_attention(q.data_ptr(), hq * hd, kc.data_ptr(), vt.data_ptr(), _lib().ptr(rk),
                                       rp.data_ptr(), n, hq, hkv, hd, smax, smax - 1, out.data_ptr(), hq * hd,
-                                      work.data_ptr(), stream_ptr()))
+                                      po.data_ptr(), plm.data_ptr(), work.data_ptr(), stream_ptr()))
         torch.cuda.synchronize()
-        assert int(work[:4].view(torch.int32).item()) == 0, "cross-block hand-off timed out"
+        assert int(work[:4].view(torch.int32).item()) == 0, "cross-chunk hand-off timed out"
     return out
 
 

@@ -66,8 +66,10 @@ _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+                              c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "zmi_attention_chunk": (c_int, []),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

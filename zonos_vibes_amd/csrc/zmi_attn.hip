@@ -13,30 +13,29 @@
 //   out   = bf16(acc * (1 / l))
 // (tests/test_oracle_golden.py::test_attention_block_structure pins this against torch's CPU SDPA.)
 //
-// Parallel form: one 1024-thread workgroup (16 waves) per (query, kv head, 512-key block); the G
-// query heads of the group share every K/V byte the block reads. Wave w owns keys 32w .. 32w+31:
+// Parallel form: one workgroup of NWC waves per (query, kv head, chunk of CH = 32 NWC keys); a
+// 512-key block is CPB = 512 / CH chunks. The G query heads of the group share every K/V byte the
+// chunk reads. Wave w owns 32 keys of the chunk:
 //   scores : v_mfma_f32_16x16x32_bf16, A = q (rows = the G heads, padded to 16), B = K rows
 //            (16 keys x 32 dims per fragment, straight from the cache);
-//   softmax: block max / exp / exp sum / bf16 P, one wave per head, through LDS;
+//   softmax: chunk max / exp / exp sum / bf16 P through LDS;
 //   P.V    : v_mfma_f32_16x16x32_bf16, A = P (16 heads x the wave's 32 keys), B = V^T fragments
 //            read straight from the transposed V cache ([dim][position]: 8 positions per lane).
-// The 16 wave partials are summed in wave order. A block needs the maxima of the blocks before
-// it (M_{j-1}): each block publishes its block maxima as 8-byte {value, tag} granules and block j
-// polls those of blocks 0..j-1 (lower workgroup ids only: the blocks of a query are consecutive
-// in the grid). The partials (o, l, M_j) are merged in block order by the last-arriving block of
-// the query, which also re-arms the tags. The result depends only on the query's position,
-// never on batch size or scheduling.
+// M_j needs the maxima of every chunk of blocks 0..j: each chunk publishes its maxima as 8-byte
+// {value, tag} granules and polls the others' (bounded spin; a give-up sets the error word).
+// The chunk partials (o, l, M_j; layout and merge order in zmi_attn_merge.h) are merged by the
+// last-arriving chunk of the query. (Deferring the merge into out_proj's prologue was measured:
+// attention 12.2 -> 9.2 us but out_proj 4.0 -> 7.8 us per layer at C2, so it is not done.) Every query runs the same
+// arithmetic whatever the batch: the result depends only on its position (CH is a constant).
 // Cache layouts: K [row][kv head][position][128], V^T [row][kv head][128][position], bf16.
 #include "zmi_common.h"
 #include "zmi_kernels.h"
+#include "zmi_attn_merge.h"
 
 namespace {
 
-constexpr int HD = 128;
-constexpr int BLK = 512;  // kvSplitSize of the reference's CPU attention
-constexpr int NW = 16;    // waves per workgroup
-constexpr int KPW = BLK / NW;
-constexpr int NT = NW * 64;
+using namespace zmi_attn;
+constexpr int NT = NWC * 64;
 constexpr unsigned SPIN_LIMIT = 1u << 20;
 
 struct AttnArgs {
@@ -46,15 +45,30 @@ struct AttnArgs {
   const bf16_t* v;
   const int* kv_row;
   const int* pos;
-  int hkv, smax, nblk;
+  int hkv, smax, nch;
   float scale;
   bf16_t* out;
   int ldo;
   unsigned* err;       // nonzero after a hand-off poll gave up
   unsigned* tickets;   // [unit]
-  uint64_t* gran;      // [unit][nblk][G]   {block max, tag}
-  float* part;         // [unit][nblk][G][HD + 2]   o[HD], l, M_j
+  uint64_t* gran;      // [unit][nch][G]   {chunk max, tag}
+  float* part_o;       // [unit][nch][G][HD]
+  float* part_lm;      // [unit][nch][G][2]   l, M_j
+  unsigned long long* stamps;  // diagnostic build only
 };
+
+// Diagnostic build only (-DZMI_ATTN_STAMPS, tools/attn_stamps.py): thread 0 of every workgroup
+// writes s_memrealtime (100 MHz) at phase boundaries into a.stamps[block][8]; the real kernel has none.
+#ifdef ZMI_ATTN_STAMPS
+#define ZMI_ASTAMP(i)                                                                                    \
+  do {                                                                                                   \
+    if (threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define ZMI_ASTAMP(i) \
+  do {                \
+  } while (0)
+#endif
 
 __device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -63,25 +77,28 @@ __device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_
 
 template <int G>
 __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
-  __shared__ float sc[G][BLK];
-  __shared__ __attribute__((aligned(16))) bf16_t pb[G][BLK];
-  __shared__ float opart[NW][G][HD];
+  __shared__ float sc[G][CH];
+  __shared__ __attribute__((aligned(16))) bf16_t pb[G][CH];
+  __shared__ float opart[NWC][G][HD];
   __shared__ float mj[G], lj[G];
+  __shared__ float pmax[NT];
   __shared__ unsigned last_flag;
 
-  const int unit = blockIdx.x / a.nblk, j = blockIdx.x - unit * a.nblk;
+  const int unit = blockIdx.x / a.nch, c = blockIdx.x - unit * a.nch;
   const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int pos = a.pos[qi];
-  if (pos < 0) return;
-  const int nb = pos / BLK + 1;
-  if (j >= nb) return;
-  const int key0 = j * BLK;
-  const int nkeys = min(BLK, pos + 1 - key0);
+  const int nc = chunks_of(pos);  // chunks of this query
+  if (c >= nc) return;
+  const int j = c / CPB;                               // its 512-key block
+  const int dep = min((j + 1) * CPB, nc);              // chunks 0 .. dep-1 make up M_j
+  const int key0 = c * CH;
+  const int nkeys = min(CH, pos + 1 - key0);
   const int kvr = a.kv_row ? a.kv_row[qi] : qi;
   const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
   const int last_key = key0 + nkeys - 1;
   const int c16 = lane & 15, h4 = lane >> 4;
+  ZMI_ASTAMP(0);
 
   // ---- q (A operand: row = head, zero rows past G) and this wave's K rows (B operand) ----
   uint4 qf[4];
@@ -97,10 +114,20 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
   uint4 kf[2][4];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const int key = min(key0 + wave * KPW + 16 * tt + c16, last_key);
+    const int key = min(key0 + wave * 32 + 16 * tt + c16, last_key);
     const bf16_t* kr = a.k + kvbase + (size_t)key * HD + 8 * h4;
 #pragma unroll
     for (int db = 0; db < 4; ++db) kf[tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
+  }
+  // V^T fragments for P.V, issued with K so both streams share one memory latency (B operand:
+  // dim = 16 dt + c16, positions 32 w + 8 h4 .. +7; groups wholly past the position re-read the
+  // last valid group, their keys are masked below)
+  uint4 vf[8];
+  {
+    const int p0 = min(key0 + wave * 32 + 8 * h4, (last_key & ~7));
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
   }
 
   // ---- scores s = fp32(q . k) * scale; keys past the position are -inf ----
@@ -109,79 +136,85 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
     f32x4_t s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int db = 0; db < 4; ++db) s = mfma16(qf[db], kf[tt][db], s);
-    const int key = wave * KPW + 16 * tt + c16;  // accumulator: column = key, row = head 4 h4 + i
+    const int key = wave * 32 + 16 * tt + c16;  // accumulator: column = key, row = head 4 h4 + i
     if (h4 == 0) {
 #pragma unroll
       for (int i = 0; i < G; ++i) sc[i][key] = key < nkeys ? s[i] * a.scale : -INFINITY;
     }
   }
-  // ---- V^T fragments for P.V (B operand: dim = 16 dt + c16, positions 32 w + 8 h4 .. +7) ----
-  __builtin_amdgcn_sched_barrier(0);
-  uint4 vf[8];
-  {
-    const int p0 = min(key0 + wave * KPW + 8 * h4, a.smax - 8);  // 8 positions stay inside the row
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-      vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
-  }
-  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
+  ZMI_ASTAMP(1);
 
-  // ---- block maxima (one wave per head) ----
-  if (wave < G) {
+  // ---- chunk maxima: a wave per head, lane scans keys lane, lane + 64 .. ----
+  for (int g = wave; g < G; g += NWC) {
     float m = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < BLK / 64; ++i) m = fmaxf(m, sc[wave][lane + 64 * i]);
+    for (int i = 0; i < CH / 64; ++i) m = fmaxf(m, sc[g][lane + 64 * i]);
     m = wave_max(m);
-    if (lane == 0) mj[wave] = m;
+    if (lane == 0) mj[g] = m;
   }
   __syncthreads();
+  ZMI_ASTAMP(2);
 
-  // ---- running maximum M_j = max(block max, maxima of blocks 0..j-1) ----
-  uint64_t* gu = a.gran + (size_t)unit * a.nblk * G;
-  if (nb > 1 && t < G) {
-    const float m = mj[t];
-    st_wt64(gu + j * G + t, pack_f2(m, 1.0f));  // {value, tag = 1.0f}: one untorn 8-byte granule
-    float mm = m;
-    for (int jj = 0; jj < j; ++jj) {
-      uint64_t v = ld_wt64(gu + jj * G + t);
+  // ---- running maximum M_j = max over the chunks of blocks 0..j: {value, tag} granule exchange ----
+  uint64_t* gu = a.gran + (size_t)unit * a.nch * G;
+  if (nc > 1 && t < G) st_wt64(gu + c * G + t, pack_f2(mj[t], 1.0f));  // {value, tag 1.0f}: untorn granule
+#ifdef ZMI_ATTN_NOEXCH  // timing experiment only: wrong numerics
+  if (false) {
+#else
+  if (dep > 1) {
+#endif
+    float m = -INFINITY;
+    for (int e = t; e < dep * G; e += NT) {  // e = chunk * G + head
+      if (e / G == c) {
+        m = fmaxf(m, mj[e % G]);
+        continue;
+      }
+      uint64_t v = ld_wt64(gu + e);
       unsigned spins = 0;
       while (hi_f(v) != 1.0f) {
         if (++spins > SPIN_LIMIT) {
           __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
-        v = ld_wt64(gu + jj * G + t);
+        v = ld_wt64(gu + e);
       }
-      mm = fmaxf(mm, lo_f(v));
+      m = fmaxf(m, lo_f(v));
     }
-    mj[t] = mm;
+    pmax[t] = m;
+    __syncthreads();
+    if (t < G) {  // thread t gathers head t: entries e = t, t + G, ... hold head t (NT % G == 0)
+      float mm = -INFINITY;
+      for (int e = t; e < NT; e += G) mm = fmaxf(mm, pmax[e]);
+      mj[t] = mm;
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  ZMI_ASTAMP(3);
 
   // ---- e = exp(s - M_j), l = sum e (fp32), P = bf16(e) ----
-  if (wave < G) {
-    const float M = mj[wave];
+  for (int g = wave; g < G; g += NWC) {
+    const float M = mj[g];
     float l = 0.f;
 #pragma unroll
-    for (int i = 0; i < BLK / 64; ++i) {
+    for (int i = 0; i < CH / 64; ++i) {
       const int kk = lane + 64 * i;
-      const float e = kk < nkeys ? expf(sc[wave][kk] - M) : 0.f;
+      const float e = kk < nkeys ? expf(sc[g][kk] - M) : 0.f;
       l += e;
-      pb[wave][kk] = (bf16_t)f2bf(e);
+      pb[g][kk] = (bf16_t)f2bf(e);
     }
     l = wave_sum(l);
-    if (lane == 0) lj[wave] = l;
+    if (lane == 0) lj[g] = l;
   }
   __syncthreads();
+  ZMI_ASTAMP(4);
 
   // ---- P.V: this wave's 32 keys x 128 dims (V of keys past the position is zeroed: never let
   // stale cache bytes into the sum) ----
   {
     uint4 pf = uint4{0u, 0u, 0u, 0u};
-    if (c16 < G) pf = *reinterpret_cast<const uint4*>(&pb[c16][wave * KPW + 8 * h4]);
-    const int kbase = wave * KPW + 8 * h4;  // first key of this lane's 8 positions
+    if (c16 < G) pf = *reinterpret_cast<const uint4*>(&pb[c16][wave * 32 + 8 * h4]);
+    const int kbase = wave * 32 + 8 * h4;  // first key of this lane's 8 positions
     if (kbase + 8 > nkeys) {
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
@@ -206,54 +239,60 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
   }
   __syncthreads();
 
-  constexpr int NOUT = G * HD;  // (head, dim) outputs; thread t < NOUT owns one
-  float o = 0.f;
-  const int g_t = t / HD, d_t = t - g_t * HD;
-  if (t < NOUT) {
-    o = opart[0][g_t][d_t];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) o += opart[w][g_t][d_t];
-  }
+  // ---- chunk partial (waves in order) ----
+  float* po = a.part_o + ((size_t)unit * a.nch + c) * G * HD;
+  float* plm = a.part_lm + ((size_t)unit * a.nch + c) * G * 2;
   bf16_t* dst = a.out + (size_t)qi * a.ldo + kh * G * HD;
-  if (nb == 1) {
-    if (t < NOUT) dst[t] = (bf16_t)f2bf(o * (1.0f / lj[g_t]));
-    return;
+  for (int e = t; e < G * HD; e += NT) {
+    const int g = e / HD, d = e - g * HD;
+    float o = opart[0][g][d];
+#pragma unroll
+    for (int w = 1; w < NWC; ++w) o += opart[w][g][d];
+    if (nc == 1)  // a one-chunk query is finished here
+      dst[e] = (bf16_t)f2bf(o * (1.0f / lj[g]));
+    else
+      st_wt(po + e, o);
   }
-
-  // ---- publish this block's partial; the last-arriving block merges in block order ----
-  float* pu = a.part + (size_t)unit * a.nblk * G * (HD + 2);
-  if (t < NOUT) st_wt(pu + ((size_t)j * G + g_t) * (HD + 2) + d_t, o);
+  if (nc == 1) return;
   if (t < G) {
-    st_wt(pu + ((size_t)j * G + t) * (HD + 2) + HD, lj[t]);
-    st_wt(pu + ((size_t)j * G + t) * (HD + 2) + HD + 1, mj[t]);
+    st_wt(plm + 2 * t, lj[t]);
+    st_wt(plm + 2 * t + 1, mj[t]);
   }
-  if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nb, &last_flag)) return;
-  if (t < nb * G) st_wt64(gu + t, 0ull);  // re-arm the granules (every block of the query has polled)
-  if (t >= NOUT) return;
-  const float* pg = pu + (size_t)g_t * (HD + 2);
-  const size_t bs = (size_t)G * (HD + 2);
-  float acc = ld_wt(pg + d_t), l = ld_wt(pg + HD), mprev = ld_wt(pg + HD + 1);
-  for (int jj = 1; jj < nb; ++jj) {
-    const float* pj = pg + jj * bs;
-    const float oj = ld_wt(pj + d_t), lb = ld_wt(pj + HD), mb = ld_wt(pj + HD + 1);
-    const float et = expf(mprev - mb);
-    l = lb + et * l;
-    acc = acc * et + oj;
-    mprev = mb;
+  ZMI_ASTAMP(5);
+  if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nc, &last_flag)) return;
+  ZMI_ASTAMP(6);
+  for (int e = t; e < nc * G; e += NT) st_wt64(gu + e, 0ull);  // re-arm (every chunk has polled)
+
+  // ---- merge (zmi_attn_merge.h), 4 dims per thread. The partials were stored write-through by
+  // their chunks; one agent-scope acquire here, then plain loads (MI355X_MICROARCH.md, Valid forms) ----
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  dst[t] = (bf16_t)f2bf(acc * (1.0f / l));
+  __syncthreads();
+  const float* ou = a.part_o + (size_t)unit * a.nch * G * HD;
+  const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
+  for (int e = t * 4; e < G * HD; e += NT * 4) {
+    const int g = e / HD, d = e - g * HD;
+    const float4 r = merge4(ou, lu, nc, g, d, G);
+    *reinterpret_cast<uint2*>(dst + e) = uint2{f2bf(r.x) | (f2bf(r.y) << 16), f2bf(r.z) | (f2bf(r.w) << 16)};
+  }
+  ZMI_ASTAMP(7);
 }
 
 struct WorkLayout {
-  size_t tickets, gran, part, total;
+  size_t tickets, gran, stamps, total;
 };
 WorkLayout work_layout(int n_query, int g, int hkv, int max_pos) {
-  const size_t units = (size_t)n_query * hkv, nblk = (size_t)max_pos / BLK + 1;
+  const size_t units = (size_t)n_query * hkv, nch = (size_t)max_pos / CH + 1;
   WorkLayout w;
   w.tickets = 256;
   w.gran = w.tickets + ((units * 4 + 255) / 256) * 256;
-  w.part = w.gran + ((units * nblk * g * 8 + 255) / 256) * 256;
-  w.total = w.part + units * nblk * g * (HD + 2) * 4;
+  w.stamps = w.gran + ((units * nch * g * 8 + 255) / 256) * 256;
+  w.total = w.stamps;
+#ifdef ZMI_ATTN_STAMPS
+  w.total += units * nch * 8 * 8;
+#endif
   return w;
 }
 
@@ -264,15 +303,22 @@ extern "C" int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd
   return (int64_t)work_layout(n_query, hq / hkv, hkv, max_pos).total;
 }
 
+extern "C" int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos) {
+  if (hd != HD || hkv <= 0 || hq % hkv || n_query <= 0 || max_pos < 0) return -1;
+  return (int64_t)n_query * hkv * (max_pos / CH + 1) * (hq / hkv) * HD;
+}
+
+extern "C" int zmi_attention_chunk(void) { return CH; }
+
 extern "C" int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                              const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
-                             int ldo, void* work, void* stream) {
+                             int ldo, float* part_o, float* part_lm, void* work, void* stream) {
   if (hd != HD) return zmi_fail_msg("attention: head_dim must be 128");
   if (max_pos >= smax) return zmi_fail_msg("attention: max_pos must be < smax");
   if (smax % 8) return zmi_fail_msg("attention: smax must be a multiple of 8");
-  if (ldq % 8) return zmi_fail_msg("attention: ldq must be a multiple of 8");
+  if (ldq % 8 || ldo % 4) return zmi_fail_msg("attention: ldq must be a multiple of 8, ldo of 4");
   if (n_query <= 0) return 0;
-  if (!work) return zmi_fail_msg("attention: work buffer required (zmi_attention_work_bytes)");
+  if (!work || !part_o || !part_lm) return zmi_fail_msg("attention: work and partial buffers required");
   const int g = hkv > 0 ? hq / hkv : 0;
   if (g * hkv != hq) return zmi_fail_msg("attention: hq must be a multiple of hkv");
   const WorkLayout w = work_layout(n_query, g, hkv, max_pos);
@@ -286,15 +332,17 @@ extern "C" int zmi_attention(const void* q, int ldq, const void* k_cache, const 
   a.pos = q_pos;
   a.hkv = hkv;
   a.smax = smax;
-  a.nblk = max_pos / BLK + 1;
+  a.nch = max_pos / CH + 1;
   a.scale = 1.0f / sqrtf((float)hd);
   a.out = (bf16_t*)out;
   a.ldo = ldo;
   a.err = (unsigned*)wb;
   a.tickets = (unsigned*)(wb + w.tickets);
   a.gran = (uint64_t*)(wb + w.gran);
-  a.part = (float*)(wb + w.part);
-  const int64_t blocks = (int64_t)n_query * hkv * a.nblk;
+  a.part_o = part_o;
+  a.part_lm = part_lm;
+  a.stamps = (unsigned long long*)(wb + w.stamps);
+  const int64_t blocks = (int64_t)n_query * hkv * a.nch;
   if (blocks > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
   hipStream_t s = (hipStream_t)stream;
   switch (g) {

@@ -115,6 +115,9 @@ class HipEngine:
             if wb < 0:
                 raise ValueError("attention geometry not supported by the HIP kernel")
             self.attn_work = z(wb, dt=torch.uint8)  # first word: hand-off timeout flag
+            nf = self.lib.zmi_attention_partial_floats(nq, self.H, self.Hkv, self.hd, self.smax - 1)
+            self.attn_o = z(nf, dt=torch.float32)        # attention chunk partials (zmi_attn_merge.h)
+            self.attn_lm = z(nf // self.hd * 2, dt=torch.float32)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -240,7 +243,8 @@ class HipEngine:
         _lib.check(self.lib.zmi_attention(q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(),
                                           _lib.ptr(row_kv), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
                                           self.smax, max_pos, out.data_ptr(), self.H * self.hd,
-                                          self.attn_work.data_ptr(), self.sptr), "attention")
+                                          self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(),
+                                          self.sptr), "attention")
 
     def check_errors(self):
         """Raise if an attention launch gave up waiting on a cross-block hand-off (bounded spin)."""
