@@ -117,6 +117,61 @@ def run_generate(model, cond, prefix, n, params, threads, seed):
                           sampling_params=params, progress_bar=False, disable_torch_compile=True)
 
 
+def ulp(x: torch.Tensor) -> torch.Tensor:
+    return torch.ldexp(torch.ones_like(x), torch.frexp(x.abs().clamp_min(1e-30))[1] - 8)
+
+
+class Fp64Linear:
+    """Context: every nn.Linear / F.linear of the reference computed exactly (fp64) and rounded to
+    its dtype once -- an implementation that differs from the reference only in the GEMMs'
+    accumulation order, to measure the logit noise such a difference alone causes."""
+    def __enter__(self):
+        import torch.nn.functional as F
+        self.orig = F.linear
+        F.linear = lambda x, w, b=None: ((x.double() @ w.double().t()) + (0 if b is None else b.double())).to(x.dtype)
+        return self
+
+    def __exit__(self, *a):
+        import torch.nn.functional as F
+        F.linear = self.orig
+
+
+def teacher_forced_scores(model, zs, cond, prefix_len, delayed, n_decisions):
+    """Reference decisions along a known delayed trajectory (model.py:240-307 with the sampled tokens
+    fixed): per decision the CFG'd logits and the scores greedy argmax sees (EOS bias + penalty)."""
+    lc = cond.shape[1]
+    logits, scores = [], []
+    with torch.inference_mode():
+        ip = model.setup_cache(batch_size=2, max_seqlen=lc + delayed.shape[-1])
+        lg = model._prefill(cond, delayed[..., : prefix_len + 1], ip, 2.0)
+        logits.append(lg[0].clone())
+        scores.append(lg[0].clone())
+        ip.seqlen_offset += lc + prefix_len + 1
+        ip.lengths_per_sample[:] += lc + prefix_len + 1
+        bias = torch.zeros_like(lg)
+        bias[:, 1:, 1024] = -torch.inf
+        offset = prefix_len + 1
+        for _ in range(n_decisions - 1):
+            offset += 1
+            lg = model._decode_one_token(delayed[..., offset - 1:offset], ip, torch.tensor(2.0),
+                                         allow_cudagraphs=False).clone()
+            logits.append(lg[0].clone())
+            scores.append(zs.modify_logit_for_repetition_penalty(lg + bias, delayed[..., :offset], 3.0, 2)[0])
+            ip.seqlen_offset += 1
+            ip.lengths_per_sample[:] += 1
+    return logits, scores
+
+
+def noise_ulps(a_list, b_list):
+    """Max |a - b| per decision and codebook, in bf16 ulps of a's top score."""
+    out = []
+    for a, b in zip(a_list, b_list):
+        fin = torch.isfinite(a)
+        top = a.masked_fill(~fin, -torch.inf).max(-1).values
+        out.append((a - b).masked_fill(~fin, 0).abs().max(-1).values / ulp(top))
+    return torch.stack(out)
+
+
 def stable(model, cond, prefix, n, params, seed=0):
     outs = [run_generate(model, cond, prefix, n, params, t, seed) for t in (1, 3, 8)]
     same = all(o.shape == outs[0].shape and torch.equal(o, outs[0]) for o in outs)
@@ -168,7 +223,7 @@ def main():
     traj_t, traj_meta = {}, {"cfg": cfg.to_dict(), "cases": []}
 
     def add_case(tag, model_kw, cond_seed, lc, n, params, prefix_len=0, seed=0, require_stable=True):
-        model, _ = build_ref_model(zm, ZonosConfig, BACKBONES, cfg, **model_kw)
+        model, w_case = build_ref_model(zm, ZonosConfig, BACKBONES, cfg, **model_kw)
         cond = cond_tensor(cond_seed, 2, lc, cfg.backbone.d_model)
         prefix = None
         if prefix_len:
@@ -181,8 +236,30 @@ def main():
         traj_t[tag + "/codes"] = out
         if prefix is not None:
             traj_t[tag + "/prefix"] = prefix
+        extra = {}
+        if params.get("temperature", 1.0) == 0.0:
+            # the reference's decisions along its own trajectory (its delayed frames from the oracle,
+            # which is bit-identical here), and the noise an exact-GEMM implementation shows on them
+            from oracle.zonos_cpu import OracleZonos
+            torch.set_num_threads(8)
+            om = OracleZonos(cfg, w_case)
+            raw = []
+            o_codes = om.generate(cond, prefix, max_new_tokens=n, sampling_params=params, raw_trace=raw)
+            assert torch.equal(o_codes, out)
+            dl = om.last_delayed
+            lg, sc = teacher_forced_scores(model, zs, cond, prefix_len, dl, len(raw))
+            with Fp64Linear():
+                lg64, _ = teacher_forced_scores(model, zs, cond, prefix_len, dl, len(raw))
+            t2 = torch.stack([x.topk(2, dim=-1).values for x in sc])
+            traj_t[tag + "/delayed"] = dl.to(torch.int16).contiguous()
+            traj_t[tag + "/top"] = t2[..., 0].contiguous()
+            traj_t[tag + "/margin"] = (t2[..., 0] - t2[..., 1]).contiguous()
+            nz = noise_ulps(lg, lg64)
+            extra = dict(exact_gemm_noise=dict(max_ulps=float(nz.max()), mean_ulps=float(nz.mean())))
+            print(tag, extra)
         traj_meta["cases"].append(dict(tag=tag, model_kw=model_kw, cond_seed=cond_seed, lc=lc, n=n, params=params,
-                                       prefix_len=prefix_len, seed=seed, threads_checked=[1, 3, 8], stable=ok))
+                                       prefix_len=prefix_len, seed=seed, threads_checked=[1, 3, 8], stable=ok,
+                                       **extra))
         return True
 
     greedy_p = dict(temperature=0.0)

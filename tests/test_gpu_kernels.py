@@ -249,7 +249,7 @@ def test_attention_is_batch_invariant():
         assert torch.equal(one[0], full[r])
 
 
-def _slots(S=4, tcap=64):
+def _slots(S=4, tcap=128):
     L = _lib()
     st = {k: torch.zeros(S, dtype=torch.int32, device=DEV) for k in
           ("active", "pos", "offset", "remaining", "stopping", "step", "total_len")}
@@ -296,6 +296,16 @@ def test_sampler_greedy_with_penalty_matches_reference():
     t, _ = load_golden("penalty_greedy")
     out, _, _ = _run_sampler_on_final_logits(t["logits"], t["generated"], dict(temperature=0.0))
     assert torch.equal(out, t["greedy"])
+
+
+def test_sampler_penalty_windows_match_reference():
+    """Windows beyond the default 2, the whole history (0) and negative windows: the kernel
+    counts every token of generated[..., -window:] (reference sampling.py:99-114)."""
+    t, meta = load_golden("penalty_windows")
+    for w in meta["windows"]:
+        out, _, _ = _run_sampler_on_final_logits(t["logits"], t["generated"],
+                                                 dict(temperature=0.0, repetition_penalty_window=w))
+        assert torch.equal(out, t[f"greedy{w}"]), w
 
 
 def test_sampler_stochastic_matches_reference_with_same_noise():

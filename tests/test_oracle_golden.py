@@ -25,6 +25,17 @@ def test_penalty_and_greedy_match_reference():
     assert torch.equal(g, t["greedy"])
 
 
+def test_penalty_windows_match_reference():
+    """Any repetition-penalty window, including 0 (the slice [..., -0:] = whole history) and
+    negative ones (Python slice semantics), sampling.py:99-114."""
+    t, meta = load_golden("penalty_windows")
+    for w in meta["windows"]:
+        pen = oz.repetition_penalty(t["logits"].clone(), t["generated"], meta["penalty"], w)
+        assert torch.equal(pen, t[f"pen{w}"]), w
+        g = oz.sample(t["logits"].clone(), temperature=0.0, generated=t["generated"], rep_window=w)
+        assert torch.equal(g, t[f"greedy{w}"]), w
+
+
 def test_samplers_match_reference_with_its_own_noise():
     t, meta = load_golden("samplers")
     for i, ps in enumerate(meta["params"]):

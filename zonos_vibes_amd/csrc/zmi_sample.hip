@@ -3,7 +3,7 @@
 // One workgroup per (codebook, slot) computes, over the 1026-entry vocabulary:
 //   CFG            u + (c - u) * cfg, column 1025 = -inf          reference model.py:112-115
 //   EOS bias       -inf on EOS for codebooks 1..8 (decode only)    model.py:266-267,280
-//   rep. penalty   3^count over the last `window` delayed tokens   sampling.py:99-114,164-165
+//   rep. penalty   penalty^count over generated[..., -window:]   sampling.py:99-114,164-165 (any window)
 //   greedy         argmax, first index on ties                      sampling.py:180
 //   stochastic     softmax(l/T) -> [unified] -> [top-p] -> [top-k] -> [min-p] -> argmax(p/q),
 //                  q ~ Exp(1) from a counter-based hash (or a caller noise buffer)  sampling.py:4-96,167-178
@@ -137,6 +137,7 @@ __device__ void softmax_inplace(float* x, float* red) {
 
 __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
   __shared__ float probs[NV + 2];
+  __shared__ int cnt[NV];
   __shared__ uint64_t keys[SORTN];
   __shared__ double dscan[256];
   __shared__ float red[4];
@@ -155,16 +156,16 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
   const int o = a.sl.offset[s] + 1;  // frame written this step
 
   // ---- CFG, padding, EOS bias, repetition penalty ----
-  int win_lo = 0, win_hi = 0;
-  if (decode && P.rep_penalty != 1.0f) {
-    win_hi = o;
-    win_lo = max(0, o - P.rep_window);
+  // window = generated_tokens[..., -window:] over the delayed frames 0 .. o-1 (Python slice
+  // semantics: window <= 0 gives [-window:], i.e. the whole history for 0); counts per token in LDS
+  const bool pen = decode && P.rep_penalty != 1.0f;
+  if (pen) {
+    const int win_lo = P.rep_window > 0 ? max(0, o - P.rep_window) : min(o, -P.rep_window);
+    for (int v = t; v < NV; v += 256) cnt[v] = 0;
+    __syncthreads();
+    for (int i = win_lo + t; i < o; i += 256) atomicAdd(&cnt[min(dl[i], NV - 1)], 1);
+    __syncthreads();
   }
-  constexpr int MAXW = 8;  // penalty window tokens held in registers (windows beyond 8 are truncated)
-  int wtok[MAXW];
-  const int nw = min(win_hi - win_lo, MAXW);
-#pragma unroll
-  for (int j = 0; j < MAXW; ++j) wtok[j] = nw > 0 ? min(dl[win_hi - nw + min(j, nw - 1)], NV - 1) : -1;
   float cv[PER], uv[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {  // all logit loads in flight together (clamped index)
@@ -180,11 +181,9 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     float l = u + (c - u) * P.cfg_scale;
     if (v >= 1025) l = -INFINITY;
     if (decode) l = l + ((cb >= 1 && v == ZMI_EOS) ? -INFINITY : 0.0f);
-    if (nw > 0) {
+    if (pen) {  // factor = penalty^count as the reference's scatter_reduce(prod) builds it
       float f = 1.0f;
-#pragma unroll
-      for (int j = 0; j < MAXW; ++j)
-        if (j < nw && wtok[j] == v) f = f * P.rep_penalty;
+      for (int k = cnt[v]; k > 0; --k) f = f * P.rep_penalty;
       l = (l <= 0.f) ? l * f : l / f;
     }
     probs[v] = l;
