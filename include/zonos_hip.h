@@ -57,6 +57,10 @@ typedef struct ZmiGemvArgs {
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
 /* One kernel for every M: a row's result is bit-identical whatever the batch it is computed in. */
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
+/* out[r] = LayerNorm(x[r]) bf16, r < m (nn.LayerNorm, _torch.py:62: norm_f for the backbone plugin),
+ * with the GEMV LayerNorm prologue's arithmetic; k in {512, 1024, 2048, 4096}. */
+int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps, void* out,
+                       int ldo, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Attention: GQA scaled-dot-product attention over the KV cache, one query position per
@@ -110,6 +114,15 @@ typedef struct ZmiSlots {
 int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
                     unsigned* counters, int mode, int slot_begin, int slot_count, const void* emb, int d, void* x,
                     int* row_kv, int* row_pos, void* stream);
+/* sample_from_logits (sampling.py:117-182) on its own: logits f32 [batch][9][1026] as given (no CFG,
+ * no EOS bias), optional generated_tokens int32 [batch][9][gen_len] for the repetition penalty,
+ * one parameter block (device), optional exponential noise [batch][9][1026]; tokens int32 [batch][9]. */
+int zmi_sample_logits(const float* logits, const int* generated, int gen_len, int batch, const ZmiSampling* params,
+                      const float* noise, int* tokens, void* stream);
+/* apply_delay_pattern / revert_delay_pattern (codebook_pattern.py:5-12) on int64 [batch][9][T]
+ * (apply: out [batch][9][T + 9]; revert: T >= 9, out [batch][9][T - 9]). */
+int zmi_apply_delay_pattern(const int64_t* codes, int64_t* out, int batch, int T, int64_t mask_token, void* stream);
+int zmi_revert_delay_pattern(const int64_t* codes, int64_t* out, int batch, int T, void* stream);
 /* x[2s], x[2s+1] = sum_k emb_k[delayed[s][k][offset[s]]]  (model.py:97-98,142) and the
  * per-row (kv row, position) tables of the step (-1 position for inactive slots). */
 int zmi_embed_step(const ZmiSlots* slots, const void* emb, int d, void* x, int* row_kv, int* row_pos,

@@ -1,13 +1,13 @@
 """zonos_vibes_amd — MI355X-native (gfx950) Zonos generate() + DAC decode hot path.
 
 Public surface mirrors the reference (BreakTheBeta/Zonos_Vibes):
-    Zonos.generate(...)           reference zonos/model.py:218-315
-    DACAutoencoder.decode(codes)  reference zonos/autoencoder.py:25-27
-    apply/revert_delay_pattern    reference zonos/codebook_pattern.py:5-12
-    sample_from_logits            reference zonos/sampling.py:117-182 (HIP sampler kernel)
-    BACKBONES["hip"]              reference zonos/backbone/__init__.py:1-12
+    Zonos.generate(...)           reference zonos/model.py:218-315            (model.py)
+    DACAutoencoder.decode(codes)  reference zonos/autoencoder.py:25-27        (autoencoder.py)
+    apply/revert_delay_pattern    reference zonos/codebook_pattern.py:5-12   (codebook_pattern.py)
+    sample_from_logits            reference zonos/sampling.py:117-182        (sampling.py)
+    BACKBONES["hip"]              reference zonos/backbone/__init__.py:1-12  (backbone.py)
 """
-from .config import BackboneConfig, PrefixConditionerConfig, ZonosConfig  # noqa: F401
+from .config import BackboneConfig, InferenceParams, PrefixConditionerConfig, ZonosConfig  # noqa: F401
 
 __version__ = "0.1.0"
 
@@ -20,4 +20,13 @@ def __getattr__(name):
     if name == "DACAutoencoder":
         from .autoencoder import DACAutoencoder
         return DACAutoencoder
+    if name in ("apply_delay_pattern", "revert_delay_pattern"):
+        from . import codebook_pattern
+        return getattr(codebook_pattern, name)
+    if name == "sample_from_logits":
+        from .sampling import sample_from_logits
+        return sample_from_logits
+    if name in ("BACKBONES", "HipZonosBackbone"):
+        from . import backbone
+        return getattr(backbone, name)
     raise AttributeError(name)

@@ -65,6 +65,8 @@ COND_EMBED, COND_VECTOR, COND_FOURIER, COND_LINEAR, COND_PASSTHROUGH = range(5)
 _SIGS = {
     "zmi_pack_weight": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "zmi_gemv_launch": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p]),
+    "zmi_layernorm_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_int,
+                                   c_void_p]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
@@ -72,6 +74,9 @@ _SIGS = {
     "zmi_attention_chunk": (c_int, []),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_sample_logits": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_apply_delay_pattern": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p]),
+    "zmi_revert_delay_pattern": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "zmi_embed_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_embed_codes": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "zmi_delay_init": (c_int, [ctypes.POINTER(Slots), c_int, c_void_p, c_int, c_int, c_void_p]),

@@ -6,7 +6,8 @@ same MFMA conv kernel (strided convs in polyphase form) plus a VQ kernel; `prepr
 multiple of 512 samples (resampling needs torchaudio, absent here: only 44.1 kHz input is taken).
 
 Weights use transformers' DacModel state_dict names (quantizer.quantizers.{i}.*, decoder.*);
-weight-norm pairs (weight_g, weight_v) are folded to plain weights at load time.
+weight-norm pairs (weight_g / weight_v, or parametrizations.weight.original0 / original1) are
+folded to plain weights at load time.
 """
 from __future__ import annotations
 
@@ -24,14 +25,19 @@ DILATIONS = syn.DAC_DILATIONS
 
 
 def _fold_weight_norm(sd: dict) -> dict:
+    """Plain conv weights from weight-norm pairs, in either of the two key styles a DAC state_dict
+    can carry: `x.weight_g` / `x.weight_v` (torch.nn.utils.weight_norm, the published checkpoint)
+    or `x.parametrizations.weight.original0` / `.original1` (torch.nn.utils.parametrizations.weight_norm,
+    what transformers' DacModel.apply_weight_norm registers): weight = g * v / ||v|| over all dims
+    but the first (dim=0, torch's default)."""
     out = dict(sd)
-    for k in list(sd):
-        if k.endswith(".weight_g"):
-            base = k[: -len(".weight_g")]
-            g, v = sd[k].float(), sd[base + ".weight_v"].float()
-            norm = v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
-            out[base + ".weight"] = g * v / norm
-            del out[k], out[base + ".weight_v"]
+    for gk, vk, base in [(k, k[: -len("_g")] + "_v", k[: -len(".weight_g")]) for k in sd if k.endswith(".weight_g")] + \
+            [(k, k[: -1] + "1", k[: -len(".parametrizations.weight.original0")])
+             for k in sd if k.endswith(".parametrizations.weight.original0")]:
+        g, v = sd[gk].float(), sd[vk].float()
+        norm = v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
+        out[base + ".weight"] = g * v / norm
+        del out[gk], out[vk]
     return out
 
 

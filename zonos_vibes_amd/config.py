@@ -3,6 +3,7 @@
 Same dataclass names and field meanings as the reference so that a `config.json`
 written for `Zonos.from_local` (reference `zonos/model.py:65-88`) loads unchanged:
 
+* `InferenceParams`         -> reference `zonos/config.py:8-25`
 * `BackboneConfig`          -> reference `zonos/config.py:28-39`
 * `PrefixConditionerConfig` -> reference `zonos/config.py:42-45`
 * `ZonosConfig.from_dict`   -> reference `zonos/config.py:48-62`
@@ -26,6 +27,24 @@ HEAD_VOCAB_PADDED = 1026  # pad_weight_ adds 1025 % 8 = 1 zero row (utils.py:12-
 DAC_HOP = 512
 DAC_SAMPLE_RATE = 44100
 ROPE_TABLE_LEN = 16384    # precompute_freqs_cis(16384, hd)  reference _torch.py:67
+
+
+@dataclass
+class InferenceParams:
+    """Decode state handed to a backbone's forward (reference zonos/config.py:8-25)."""
+    max_seqlen: int
+    max_batch_size: int
+    seqlen_offset: int = 0
+    batch_size_offset: int = 0
+    key_value_memory_dict: dict = field(default_factory=dict)
+    lengths_per_sample: Any = None
+
+    def reset(self, max_seqlen: int, max_batch_size: int):
+        self.max_seqlen = max_seqlen
+        self.max_batch_size = max_batch_size
+        self.seqlen_offset = 0
+        if self.lengths_per_sample is not None:
+            self.lengths_per_sample.zero_()
 
 
 @dataclass

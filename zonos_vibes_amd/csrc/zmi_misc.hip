@@ -70,3 +70,79 @@ extern "C" int zmi_graph_destroy(void* graph_exec) {
   if (graph_exec) ZMI_CHECK(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return 0;
 }
+
+// ---- LayerNorm of whole rows (nn.LayerNorm, reference zonos/backbone/_torch.py:62,88,90) -------------
+// One wave per row with the GEMV prologue's arithmetic (zmi_gemv_impl.h step 3): lane owns the 8-element
+// chunks lane + 64 i, fp32 two-pass statistics reduced by DPP in a fixed order, bf16 output. Used for
+// norm_f by the backbone plugin (zonos_vibes_amd/backbone.py); the decode step fuses its LayerNorms.
+namespace {
+template <int CPL>
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const bf16_t* x, int ldx, int m, const bf16_t* w,
+                                                             const bf16_t* b, float eps, bf16_t* out, int ldo) {
+  constexpr int K = CPL * 512;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= m) return;
+  const bf16_t* xr = x + (size_t)r * ldx;
+  uint4 xv[CPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    xv[i] = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
+    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t += bf2f(u[j]) + bf2f(u[j] >> 16);
+    s += t;
+  }
+  const float mean = wave_sum(s) / (float)K;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
+      t += d0 * d0 + d1 * d1;
+    }
+    ss += t;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)K + eps), nbias = -mean * rstd;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
+    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+    const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float y0 = (bf2f(u[j]) * rstd + nbias) * bf2f(uw[j]) + bf2f(ub[j]);
+      const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
+      o[j] = f2bf(y0) | (f2bf(y1) << 16);
+    }
+    reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+}  // namespace
+
+extern "C" int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps,
+                                  void* out, int ldo, void* stream) {
+  if (ldx % 8 || ldo % 8) return zmi_fail_msg("layernorm_rows: ldx and ldo must be multiples of 8");
+  if (m <= 0) return 0;
+  const dim3 grid((m + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+  switch (k) {
+    case 512: hipLaunchKernelGGL(layernorm_rows_kernel<1>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, m,
+                                 (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo); break;
+    case 1024: hipLaunchKernelGGL(layernorm_rows_kernel<2>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, m,
+                                  (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo); break;
+    case 2048: hipLaunchKernelGGL(layernorm_rows_kernel<4>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, m,
+                                  (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo); break;
+    case 4096: hipLaunchKernelGGL(layernorm_rows_kernel<8>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, m,
+                                  (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo); break;
+    default: return zmi_fail_msg("layernorm_rows: k must be 512, 1024, 2048 or 4096");
+  }
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

@@ -32,6 +32,11 @@ struct SampleArgs {
   bf16_t* x;
   int* row_kv;
   int* row_pos;
+  // standalone sample_from_logits (mode 2): logits [B][9][NV] as given (no CFG), generated tokens
+  // [B][9][gen_len] int32 (or NULL), one shared parameter block; tokens to next [B][9] only
+  const int* gen;
+  int gen_len;
+  const ZmiSampling* params1;
 };
 
 __device__ void embed_row(const int* toks, const bf16_t* emb, int d, bf16_t* out0, bf16_t* out1);
@@ -145,20 +150,23 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
   __shared__ int redi[4];
   __shared__ unsigned last_flag;
 
-  const int cb = blockIdx.x, s = a.slot_begin + blockIdx.y, t = threadIdx.x;
-  if (!a.sl.active[s]) return;
-  const ZmiSampling P = a.sl.params[s];
-  const int lrow = 2 * blockIdx.y;
+  const int cb = blockIdx.x, t = threadIdx.x;
+  const bool alone = a.mode == 2;
+  const int s = alone ? blockIdx.y : a.slot_begin + blockIdx.y;
+  if (!alone && !a.sl.active[s]) return;
+  const ZmiSampling P = alone ? *a.params1 : a.sl.params[s];
+  const int lrow = alone ? blockIdx.y : 2 * blockIdx.y;
   const float* lc = a.logits + ((size_t)lrow * ZMI_NCB + cb) * NV;
-  const float* lu = a.logits + ((size_t)(lrow + 1) * ZMI_NCB + cb) * NV;
+  const float* lu = alone ? lc : a.logits + ((size_t)(lrow + 1) * ZMI_NCB + cb) * NV;
   const bool decode = a.mode == 0;
-  const int* dl = a.sl.delayed + ((size_t)s * ZMI_NCB + cb) * a.sl.tcap;
-  const int o = a.sl.offset[s] + 1;  // frame written this step
+  const int* dl = alone ? a.gen + ((size_t)s * ZMI_NCB + cb) * a.gen_len
+                        : a.sl.delayed + ((size_t)s * ZMI_NCB + cb) * a.sl.tcap;
+  const int o = alone ? a.gen_len : a.sl.offset[s] + 1;  // frames before the one sampled now
 
   // ---- CFG, padding, EOS bias, repetition penalty ----
   // window = generated_tokens[..., -window:] over the delayed frames 0 .. o-1 (Python slice
   // semantics: window <= 0 gives [-window:], i.e. the whole history for 0); counts per token in LDS
-  const bool pen = decode && P.rep_penalty != 1.0f;
+  const bool pen = (decode || (alone && a.gen)) && P.rep_penalty != 1.0f;
   if (pen) {
     const int win_lo = P.rep_window > 0 ? max(0, o - P.rep_window) : min(o, -P.rep_window);
     for (int v = t; v < NV; v += 256) cnt[v] = 0;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     const int v = t + i * 256;
     if (v >= NV) break;
     const float c = cv[i], u = uv[i];
-    float l = u + (c - u) * P.cfg_scale;
+    float l = alone ? c : u + (c - u) * P.cfg_scale;
     if (v >= 1025) l = -INFINITY;
     if (decode) l = l + ((cb >= 1 && v == ZMI_EOS) ? -INFINITY : 0.0f);
     if (pen) {  // factor = penalty^count as the reference's scatter_reduce(prod) builds it
@@ -270,7 +278,8 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
       renormalize(probs, red);
     }
     // exponential race: argmax(p / q), q ~ Exp(1)  (sampling.py:19-21)
-    const uint64_t ctr_base = ((uint64_t)(decode ? a.sl.step[s] + 1 : 0) * ZMI_NCB + cb) * NV;
+    const uint64_t ctr_base = ((uint64_t)(decode ? a.sl.step[s] + 1 : 0) * ZMI_NCB + cb) * NV +
+                              (alone ? (uint64_t)s * ZMI_NCB * NV : 0);
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int v = t; v < NV; v += 256) {
@@ -291,6 +300,10 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     tok = block_argmax(bv, bi, redv, redi);
   }
 
+  if (alone) {
+    if (t == 0) a.next[(size_t)s * ZMI_NCB + cb] = tok;
+    return;
+  }
   if (t == 0) st_wt(a.next + (size_t)s * ZMI_NCB + cb, tok);
   if (!zmi_last_arriver_wt(a.counters + s, ZMI_NCB, &last_flag)) return;
 
@@ -434,11 +447,62 @@ __global__ void delay_revert_kernel(const ZmiSlots sl, int slot, int64_t* out, i
   out[(size_t)k * t_out + t] = v >= 1024 ? 0 : v;
 }
 
+// standalone apply / revert over [B][9][T] int64 tensors (codebook_pattern.py:5-12)
+__global__ void apply_delay_kernel(const int64_t* codes, int64_t* out, int T, int64_t mask) {
+  const int t = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y, b = blockIdx.z;
+  if (t >= T + ZMI_NCB) return;
+  const int src = t - k - 1;  // roll by k + 1 of the mask-padded row
+  out[((size_t)b * ZMI_NCB + k) * (T + ZMI_NCB) + t] =
+      (src >= 0 && src < T) ? codes[((size_t)b * ZMI_NCB + k) * T + src] : mask;
+}
+
+__global__ void revert_delay_kernel(const int64_t* codes, int64_t* out, int T) {
+  const int t = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y, b = blockIdx.z;
+  if (t >= T - ZMI_NCB) return;
+  out[((size_t)b * ZMI_NCB + k) * (T - ZMI_NCB) + t] = codes[((size_t)b * ZMI_NCB + k) * T + t + k + 1];
+}
+
 }  // namespace
+
+extern "C" int zmi_apply_delay_pattern(const int64_t* codes, int64_t* out, int batch, int T, int64_t mask_token,
+                                       void* stream) {
+  if (batch <= 0 || T < 0) return zmi_fail_msg("apply_delay_pattern: bad shape");
+  hipLaunchKernelGGL(apply_delay_kernel, dim3((T + ZMI_NCB + 255) / 256, ZMI_NCB, batch), dim3(256), 0,
+                     (hipStream_t)stream, codes, out, T, mask_token);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_revert_delay_pattern(const int64_t* codes, int64_t* out, int batch, int T, void* stream) {
+  if (batch <= 0 || T < ZMI_NCB) return zmi_fail_msg("revert_delay_pattern: bad shape");
+  if (T == ZMI_NCB) return 0;
+  hipLaunchKernelGGL(revert_delay_kernel, dim3((T - ZMI_NCB + 255) / 256, ZMI_NCB, batch), dim3(256), 0,
+                     (hipStream_t)stream, codes, out, T);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_sample_logits(const float* logits, const int* generated, int gen_len, int batch,
+                                 const ZmiSampling* params, const float* noise, int* tokens, void* stream) {
+  if (batch <= 0) return 0;
+  if (!params || !tokens || !logits || (generated && gen_len <= 0)) return zmi_fail_msg("sample_logits: arguments");
+  SampleArgs a = {};
+  a.logits = logits;
+  a.noise = noise;
+  a.next = tokens;
+  a.mode = 2;
+  a.gen = generated;
+  a.gen_len = generated ? gen_len : 0;
+  a.params1 = params;
+  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, batch), dim3(256), 0, (hipStream_t)stream, a);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
 
 extern "C" int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
                                unsigned* counters, int mode, int slot_begin, int slot_count, const void* emb, int d,
                                void* x, int* row_kv, int* row_pos, void* stream) {
+  if (mode != 0 && mode != 1) return zmi_fail_msg("sample: mode must be 0 (decode) or 1 (prefill)");
   if (slot_begin < 0 || slot_begin + slot_count > slots->n_slots) return zmi_fail_msg("sample: slot range");
   if (emb && (d % 8 || !x)) return zmi_fail_msg("sample: fused embedding needs x and d % 8 == 0");
   if (!row_kv != !row_pos) return zmi_fail_msg("sample: row_kv and row_pos go together");

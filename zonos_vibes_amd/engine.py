@@ -150,7 +150,9 @@ class HipEngine:
         """Reference state_dict names (model.py:22-51, _torch.py:52-152); heads [1025, d] or [1026, d]."""
         bf = lambda t: t.to(self.dev, torch.bfloat16).contiguous()  # noqa: E731
         with torch.cuda.stream(self.stream):
-            w = {"emb": torch.stack([bf(sd[f"embeddings.{k}.weight"])[:EMB_VOCAB] for k in range(N_CODEBOOKS)])}
+            w = {}
+            if "embeddings.0.weight" in sd:  # absent for a backbone-only load (backbone.py)
+                w["emb"] = torch.stack([bf(sd[f"embeddings.{k}.weight"])[:EMB_VOCAB] for k in range(N_CODEBOOKS)])
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
             layers = []
             for i in range(self.L):
@@ -164,12 +166,13 @@ class HipEngine:
                     fc2=self._pack(sd[p + "mlp.fc2.weight"], self.d)))
             w["layers"] = layers
             w["nf_w"], w["nf_b"] = bf(sd["backbone.norm_f.weight"]), bf(sd["backbone.norm_f.bias"])
-            heads = torch.zeros(HEADS_N, self.d, dtype=torch.bfloat16, device=self.dev)
-            for k in range(N_CODEBOOKS):
-                hw = bf(sd[f"heads.{k}.weight"])[:HEAD_VOCAB]
-                heads[k * 1026: k * 1026 + HEAD_VOCAB] = hw
-            w["heads"] = self._pack(heads, HEADS_N_PAD)
-            del heads
+            if "heads.0.weight" in sd:
+                heads = torch.zeros(HEADS_N, self.d, dtype=torch.bfloat16, device=self.dev)
+                for k in range(N_CODEBOOKS):
+                    hw = bf(sd[f"heads.{k}.weight"])[:HEAD_VOCAB]
+                    heads[k * 1026: k * 1026 + HEAD_VOCAB] = hw
+                w["heads"] = self._pack(heads, HEADS_N_PAD)
+                del heads
         self.stream.synchronize()
         self.w = w
         self._build_plan()
