@@ -64,14 +64,22 @@ def time_dominant_kernel(model, reps: int = 3):
     return us, bytes_launch
 
 
+FC1_KERNEL = "gemv_kernel<2, 2, 16, 16, 1, 3, 1>"  # G, W, NL, RT, PRO_LN, EPI_SWIGLU, non-temporal
+
+
 def pmc_traffic():
-    """HBM bytes per fc1 launch from the committed FETCH_SIZE pass (tools/pmc_fc1.py; a counter pass
-    serialises dispatches, so it is not repeated inside the timed run). None if absent."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_fc1.json")
+    """HBM bytes per fc1 launch from the committed FETCH_SIZE pass of THIS kernel (tools/prof_round.sh:
+    rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950 correction; a counter pass
+    serialises dispatches, so it is not repeated inside the timed run). None when the profile is
+    absent or measured another kernel."""
+    path = os.path.join(REPO, "profiles", "r02_pmc_fc1_fetch.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return int(json.load(f)["hbm_bytes_per_launch"])
+        d = json.load(f)
+    if not d.get("kernels") or any(FC1_KERNEL not in k for k in d["kernels"]):
+        return None
+    return int(d["FETCH_SIZE_bytes_per_launch"])
 
 
 def time_decode_step(model, cond, steps: int = 64):
@@ -193,31 +201,46 @@ def step_bytes(model, pos: int) -> int:
     return w + kv
 
 
+def cpu_cores() -> int:
+    """CPU threads available to this process: its affinity set, capped by OMP_NUM_THREADS when the host
+    sets one (the GPU box gives each GPU a 16-thread share and sets OMP_NUM_THREADS=16)."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
+
+
 def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
-    """The oracle (PyTorch eager CPU, same op order as the reference) on a bounded sample of C2."""
+    """The oracle (PyTorch eager CPU, same op order as the reference) on a bounded sample of C2: the
+    prefill (2 x 161 rows), decode steps around the C2 mean position (p ~ 591) with the KV cache
+    filled to there, and DAC decode frames; extrapolated to the whole utterance."""
     from oracle.dac_cpu import OracleDAC
     from oracle.zonos_cpu import OracleZonos, apply_delay_pattern
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = cpu_cores()
     torch.set_num_threads(threads)
     w = {k: v.cpu() for k, v in dev_weights.items()}
     m = OracleZonos(cfg, w)
     cond = cond_tensor(1, cfg.backbone.d_model, "cpu")
+    mean_pos = LC + 1 + (N_NEW + 8) // 2
     with torch.inference_mode():
         cache = m.new_cache(2, LC + N_NEW + 9)
         delayed = apply_delay_pattern(torch.full((1, 9, N_NEW), -1), 1025)
         t0 = time.perf_counter()
         m.prefill(cond, delayed[..., :1], cache, 2.0)
         t_pre = time.perf_counter() - t0
-        cache["offset"] += LC + 1
-        cache["lengths"][:] += LC + 1
+        for kv in cache["kv"]:  # positions up to the sample window hold cache values (cost is data-independent)
+            kv[:, LC + 1: mean_pos + 32].normal_()
+        n_pre = mean_pos - 16
+        cache["offset"] = n_pre
+        cache["lengths"][:] = n_pre
         n, t0 = 0, time.perf_counter()
         ids = torch.randint(0, 1024, (1, 9, 1))
-        while n < 8 or (time.perf_counter() - t0 < budget_s * 0.6 and n < 200):
+        while n < 8 or (time.perf_counter() - t0 < budget_s * 0.6 and n < 32):
             m.decode_one(ids, cache, torch.tensor(2.0))
             cache["offset"] += 1
             cache["lengths"][:] += 1
             n += 1
         t_step = (time.perf_counter() - t0) / n
+        p_lo, p_hi = n_pre, n_pre + n - 1
         dac = OracleDAC({k: v for k, v in _dac_weights_cpu().items()})
         nf = 43
         t0 = time.perf_counter()
@@ -227,9 +250,10 @@ def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
     audio = N_NEW * DAC_HOP / DAC_SAMPLE_RATE
     return {"value": round(audio / total, 4), "unit": "x realtime (audio s / CPU s), extrapolated",
             "cores": threads, "kind": "port",
-            "sample": f"C2 prefill (2x{LC + 1} rows) {t_pre:.2f}s + {n} of {N_NEW + 8} decode steps "
-                      f"({t_step * 1e3:.1f} ms/step) + DAC decode of {nf} of {N_NEW} frames "
-                      f"({t_dac * 1e3:.1f} ms/frame), extrapolated to the full utterance"}
+            "sample": f"C2 prefill (2x{LC + 1} rows) {t_pre:.2f}s + {n} decode steps at positions {p_lo}..{p_hi} "
+                      f"(C2 mean {mean_pos}; {t_step * 1e3:.1f} ms/step, x{N_NEW + 8}) + DAC decode of {nf} of "
+                      f"{N_NEW} frames ({t_dac * 1e3:.1f} ms/frame), extrapolated to the full utterance; "
+                      f"{threads} threads = this process's CPU share"}
 
 
 def _dac_weights_cpu():
@@ -336,7 +360,7 @@ def main():
             "roofline": {"kernel": "gemv_kernel<G=2,W=2,NL=16,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
-                         "traffic_source": "profiles/r01_pmc_fc1.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "traffic_source": "profiles/r02_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "utterance_breakdown": breakdown,
             "widened": widened,
