@@ -229,12 +229,12 @@ def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
         t_pre = time.perf_counter() - t0
         for kv in cache["kv"]:  # positions up to the sample window hold cache values (cost is data-independent)
             kv[:, LC + 1: mean_pos + 32].normal_()
-        n_pre = mean_pos - 16
+        n_pre = mean_pos - 100  # decode steps centred on the mean position: 100 either side at most
         cache["offset"] = n_pre
         cache["lengths"][:] = n_pre
         n, t0 = 0, time.perf_counter()
         ids = torch.randint(0, 1024, (1, 9, 1))
-        while n < 8 or (time.perf_counter() - t0 < budget_s * 0.6 and n < 32):
+        while n < 8 or (time.perf_counter() - t0 < budget_s * 0.6 and n < 200):
             m.decode_one(ids, cache, torch.tensor(2.0))
             cache["offset"] += 1
             cache["lengths"][:] += 1
@@ -242,7 +242,7 @@ def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
         t_step = (time.perf_counter() - t0) / n
         p_lo, p_hi = n_pre, n_pre + n - 1
         dac = OracleDAC({k: v for k, v in _dac_weights_cpu().items()})
-        nf = 43
+        nf = 215
         t0 = time.perf_counter()
         dac.decode(torch.randint(0, 1024, (1, 9, nf)))
         t_dac = (time.perf_counter() - t0) / nf

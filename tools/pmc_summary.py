@@ -1,6 +1,7 @@
 """Counter CSV of a rocprofv3 --pmc pass -> one JSON summary per kernel (average per dispatch).
 
     python tools/pmc_summary.py <counter_collection.csv> <kernel substring> <algorithmic bytes/launch> > out.json
+    python tools/pmc_summary.py --mfma <counter_collection.csv> > out.json   (MFMA-busy pass, per kernel)
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB by rocprofv3. On gfx950 FETCH_SIZE tallies wide
 (16 B/lane) streaming reads at half their bytes (MI355X_MICROARCH.md, HBM section), so the HBM
@@ -33,5 +34,46 @@ def main(path, kernel_sub, algo_bytes):
     print(json.dumps(out, indent=1))
 
 
+def _short(name: str) -> str:
+    """Kernel name without return type, namespaces and argument list (template arguments kept)."""
+    name = name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    depth, cut, ns = 0, len(name), 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+        elif ch == ":" and depth == 0 and name[i - 1] == ":":
+            ns = i + 1
+    return name[ns:cut]
+
+
+def mfma(path):
+    """mfma_busy_frac = sum SQ_VALU_MFMA_BUSY_CYCLES / (sum GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
+    (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 256 CUs x 4 SIMDs); cu_busy_frac likewise from
+    SQ_BUSY_CU_CYCLES over 256 CUs x 4 (the counter is in quad-cycles per CU)."""
+    per = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    dur = defaultdict(dict)
+    for row in csv.DictReader(open(path)):
+        k = _short(row["Kernel_Name"])
+        per[k][row["Counter_Name"]] += float(row["Counter_Value"])
+        disp[k].add(row["Dispatch_Id"])
+        dur[k][row["Dispatch_Id"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3
+    out = {}
+    for k, c in sorted(per.items(), key=lambda kv: -sum(dur[kv[0]].values())):
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0) / 8
+        out[k] = {"dispatches": len(disp[k]), "total_us": round(sum(dur[k].values()), 1),
+                  "mfma_busy_frac": round(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (gui * 1024), 4) if gui else None,
+                  "cu_busy_frac": round(c.get("SQ_BUSY_CU_CYCLES", 0.0) * 4 / (gui * 256 * 4), 3) if gui else None}
+    print(json.dumps({"kernels": out}, indent=1))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]))
+    if sys.argv[1] == "--mfma":
+        mfma(sys.argv[2])
+    else:
+        main(sys.argv[1], sys.argv[2], int(sys.argv[3]))

@@ -25,6 +25,7 @@ pmc FETCH_SIZE attn attn_kernel 2424832 attn_fetch || exit $?
 pmc WRITE_SIZE attn attn_kernel 2424832 attn_write || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
   --output-format csv -d gpurun_out/pmc_dac -o pmc -- python tools/bench_dac.py 861 > $K/pmc_dac.log 2>&1 || exit $?
-find gpurun_out/pmc_dac -name "*counter_collection.csv" -exec cp {} $K/dac_counters.csv \;
+python tools/pmc_summary.py --mfma "$(find gpurun_out/pmc_dac -name "*counter_collection.csv" -print -quit)" \
+  > $K/dac_mfma_pmc.json || exit $?
 rm -rf gpurun_out/pmc_dac
 ls -la $K
