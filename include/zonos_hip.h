@@ -52,6 +52,7 @@ typedef struct ZmiGemvArgs {
   void* v_cache;        /* QKV: bf16 V cache, transposed: [rows][hkv][hd][smax]                 */
   int smax, hq, hkv, hd;
   const float* rope;    /* [16384][hd/2][2] (cos, sin) fp32 (_torch.py:9-15)                  */
+  void* diag;           /* NULL; diagnostic builds only (-DZMI_GEMV_STAMPS): phase stamps       */
 } ZmiGemvArgs;
 
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);

@@ -30,7 +30,7 @@ class GemvArgs(ctypes.Structure):
         ("row_kv", c_void_p), ("row_pos", c_void_p),
         ("k_cache", c_void_p), ("v_cache", c_void_p),
         ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
-        ("rope", c_void_p),
+        ("rope", c_void_p), ("diag", c_void_p),
     ]
 
 

@@ -342,9 +342,9 @@ extern "C" int zmi_attention(const void* q, int ldq, const void* k_cache, const 
   a.part_o = part_o;
   a.part_lm = part_lm;
   a.stamps = (unsigned long long*)(wb + w.stamps);
+  hipStream_t s = (hipStream_t)stream;
   const int64_t blocks = (int64_t)n_query * hkv * a.nch;
   if (blocks > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
-  hipStream_t s = (hipStream_t)stream;
   switch (g) {
     case 1: hipLaunchKernelGGL(attn_kernel<1>, dim3((unsigned)blocks), dim3(NT), 0, s, a); break;
     case 2: hipLaunchKernelGGL(attn_kernel<2>, dim3((unsigned)blocks), dim3(NT), 0, s, a); break;

@@ -62,6 +62,23 @@ struct Img {
   }
 };
 
+// Diagnostic build only (-DZMI_GEMV_STAMPS, tools/gemv_stamps.py): thread 0 of every workgroup
+// writes s_memrealtime (100 MHz) at phase boundaries into diag[reserved][block][8].
+#ifdef ZMI_GEMV_STAMPS
+#define ZMI_GSTAMP(i)                                                                              \
+  do {                                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
+    if (threadIdx.x == 0 && a.diag)                                                                \
+      reinterpret_cast<unsigned long long*>(a.diag)[((size_t)a.reserved * 4096 + blockIdx.x) * 8 + (i)] = \
+          __builtin_amdgcn_s_memrealtime();                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
+  } while (0)
+#else
+#define ZMI_GSTAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
 __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt) {
   constexpr int K = W * NL * 64;
@@ -76,6 +93,7 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
   const int idx = b >> 3;
   const int cb = (idx / n_rt) * 8 + (b & 7), rt = idx - (idx / n_rt) * n_rt;
   if (cb >= n_cb) return;  // padding block: exits before any barrier
+  ZMI_GSTAMP(0);
   const int alloc_rows = a.M < RT ? a.M : RT;
   const int row0 = rt * RT;
   const int rows = min(RT, a.M - row0);
@@ -141,47 +159,51 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
 #pragma unroll
   for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, NTW ? 2 : 0);
   __builtin_amdgcn_sched_barrier(0);
+  ZMI_GSTAMP(1);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // DMA pieces + epilogue operands landed
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  ZMI_GSTAMP(2);
 
   // (3) LayerNorm, one wave per row: lane owns the 8-element chunks lane + 64 i of the row; fp32
   // sums in a fixed lane order, DPP wave reduction, bf16-rounded result written back in place.
+  // Each pass re-reads its chunks from LDS (no row copy in VGPRs: the weight slice in flight
+  // already holds 4 NL of them, and occupancy decides whether every workgroup of a wide GEMV is
+  // resident at once).
   if (PRO == PRO_LN) {
     constexpr int CPL = K / 512;
     for (int r = wave; r < rows; r += NWV) {
       bf16_t* xr = xs + r * XROW;
-      uint4 xv[CPL];
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        xv[i] = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
-        const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t += bf2f(u[j]) + bf2f(u[j] >> 16);
-        s += t;
-      }
-      const float mean = wave_sum(s) / (float)K;
-      float ss = 0.f;
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+      auto chunk_sum = [&](int i, float mean, bool sq) {
+        const uint4 xv = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
+        const uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
         float t = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
-          t += d0 * d0 + d1 * d1;
+          if (sq) {
+            const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
+            t += d0 * d0 + d1 * d1;
+          } else {
+            t += bf2f(u[j]) + bf2f(u[j] >> 16);
+          }
         }
-        ss += t;
-      }
+        return t;
+      };
+      float s = 0.f;
+#pragma unroll 2
+      for (int i = 0; i < CPL; ++i) s += chunk_sum(i, 0.f, false);
+      const float mean = wave_sum(s) / (float)K;
+      float ss = 0.f;
+#pragma unroll 2
+      for (int i = 0; i < CPL; ++i) ss += chunk_sum(i, mean, true);
       const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)K + a.eps), nbias = -mean * rstd;
-#pragma unroll
+#pragma unroll 2
       for (int i = 0; i < CPL; ++i) {
         const int c = lane + 64 * i;
+        const uint4 xv = *reinterpret_cast<const uint4*>(xr + c * 8);
         const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
         const uint4 gb = *reinterpret_cast<const uint4*>(bet + c * 8);
-        uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+        uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
         const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -194,6 +216,7 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
     }
     __syncthreads();
   }
+  ZMI_GSTAMP(3);
 
   // (4) MFMA chain over this wave's k-segment. A operand: lane l reads row l & 15 (rows past the
   // tile re-read its last row; those outputs are discarded), k = 8 (l >> 4) .. +7 of the k-half.
@@ -210,6 +233,7 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), wv, acc1, 0, 0, 0);
     }
   }
+  ZMI_GSTAMP(4);
   // (5) segment sum = k-half 0 (tile columns 0..7) + k-half 1 (tile columns 8..15, moved down by
   // DPP); accumulator element q of lane l is row 4 (l >> 4) + q, column l & 15
   {
@@ -221,6 +245,7 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
     }
   }
   __syncthreads();
+  ZMI_GSTAMP(5);
   if (!ew) return;
   auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
     float v = red[((gi * W) * 8 + c) * RT + r];
@@ -290,6 +315,7 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
       }
     }
   }
+  ZMI_GSTAMP(6);
 }
 
 // (W, NL, RT) from K: K = 64 W NL. The LayerNorm'd K = 2048 projections stream 16 chunks per lane
