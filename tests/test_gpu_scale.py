@@ -1,0 +1,144 @@
+"""Batch sizes and context lengths of the BASELINE configs beyond C2 (MI355X only).
+
+  * C3-style continuous batching: generate_batch at 8, 16 and 64 slots gives, per utterance, the
+    codes generate() gives alone (the reference decodes batch_size=1, model.py:194;
+    every decode kernel's per-row arithmetic is independent of the row count).
+  * C5-style long context: a 430-frame audio prefix and 1,000 new frames (positions to ~1,470, four
+    512-key softmax blocks merged) through a reduced-depth model at full width, teacher-forced along
+    the oracle's own greedy trajectory (oracle/zonos_cpu.py restates model.py:218-315).
+  * C5 KV capacity: 8 slots x 5,784 positions at the full 26-layer dims, one graph-captured decode
+    step at positions ~5,770.
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from zonos_vibes_amd.config import tiny_transformer, transformer_config, zonos_v01_transformer
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cond(seed, lc, d):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(2, lc, d, generator=g) * 0.5).to(torch.bfloat16)
+
+
+def test_generate_batch_many_slots_equals_single():
+    from zonos_vibes_amd.model import Zonos
+    cfg = tiny_transformer(2)
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=96, max_prefill=32)
+    n_utt = 70
+    conds = [_cond(100 + i, 6 + i % 11, cfg.backbone.d_model).to(DEV) for i in range(n_utt)]
+    lens = [8 + (7 * i) % 33 for i in range(n_utt)]
+    params = dict(temperature=0.0)
+    single = [m.generate(c, max_new_tokens=n, sampling_params=params, progress_bar=False) for c, n in zip(conds, lens)]
+    for slots in (8, 16, 64):
+        batch = m.generate_batch(conds, max_new_tokens=lens, sampling_params=params, max_slots=slots)
+        for i, (a, b) in enumerate(zip(single, batch)):
+            assert torch.equal(a, b), (slots, i)
+    # generate() after the engine grew to 64 slots still decodes one slot pair the same way
+    again = m.generate(conds[5], max_new_tokens=lens[5], sampling_params=params, progress_bar=False)
+    assert torch.equal(again, single[5])
+
+
+def _ulp(x):
+    return torch.ldexp(torch.ones_like(x), torch.frexp(x.abs().clamp_min(1e-30))[1] - 8)
+
+
+LONG_BOUND_ULPS = 6.0  # allowed |GPU - oracle| score of the oracle's choice, bf16 ulps of its top score
+
+
+def test_long_context_prefix_430_generate_1000_teacher_forced():
+    """Full-width (d 2048, 16 / 4 heads x 128), 2 layers, Lc 32, P = 430 prefix frames, 1,000 new
+    frames, greedy with the repetition penalty, EOS suppressed. Along the oracle's trajectory every
+    decision's GPU score of the oracle's token is within LONG_BOUND_ULPS of the oracle's top score,
+    and the GPU picks the oracle's token wherever the oracle's margin exceeds twice that."""
+    from oracle.zonos_cpu import OracleZonos, apply_delay_pattern, repetition_penalty
+    from tests.helpers import synthetic_weights
+    from zonos_vibes_amd.engine import SamplingParams
+    from zonos_vibes_amd.model import Zonos
+    cfg = transformer_config(2048, 2, 16, 4, 8192)
+    lc, p, n = 32, 430, 1000
+    cond = _cond(7, lc, cfg.backbone.d_model)
+    g = torch.Generator().manual_seed(8)
+    prefix = torch.randint(0, 1024, (1, 9, p), generator=g)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    om = OracleZonos(cfg, synthetic_weights(cfg, zero_eos=True))
+    trace = []
+    om.generate(cond, prefix, max_new_tokens=n, sampling_params=dict(temperature=0.0), trace=trace)
+    dl = om.last_delayed[0].long()
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=lc + p + n + 24, max_prefill=lc + p + 8)
+    e = m.engine
+    e.prefill(0, cond.to(DEV), prefix, n, SamplingParams(temperature=0.0))
+    e.stream.synchronize()
+
+    def cfg_logits(rows):
+        c, u = rows[0].float().cpu(), rows[1].float().cpu()
+        lg = u + (c - u) * 2.0
+        lg[..., 1025:] = -torch.inf
+        return lg
+
+    bias = torch.zeros(9, 1026)
+    bias[1:, 1024] = -torch.inf
+    scores = [cfg_logits(e.logits_pre)]
+    dl_dev = dl.to(DEV, torch.int32)
+    for _ in range(len(trace) - 1):
+        with torch.cuda.stream(e.stream):  # the oracle's frames, whatever the GPU sampler chose
+            e.delayed[0, :, : dl.shape[-1]] = dl_dev
+            for k, v in (("active", 1), ("stopping", 0), ("remaining", 2000)):
+                e.st[k][0] = v
+            e.refresh_inputs()
+        o = int(e.st["offset"][0].item())
+        e.step(1, use_graph=False, slots=1)
+        e.stream.synchronize()
+        lg = cfg_logits(e.logits[0:2]) + bias
+        scores.append(repetition_penalty(lg.unsqueeze(0), dl[None, :, : o + 1], 3.0, 2)[0])
+    e.check_errors()
+    init = apply_delay_pattern(torch.cat([prefix, torch.full((1, 9, n), -1)], -1), 1025)[0]
+    rows = []
+    for i in range(min(len(trace), init.shape[1] - p - 1)):
+        f = p + 1 + i  # decision i fills the unknown codebooks of delayed frame f, in order
+        ref = trace[i][0]
+        for mm, k in enumerate((init[:, f] == -1).nonzero().flatten().tolist()):
+            tok = int(dl[k, f])
+            if tok >= 1024:
+                continue
+            t2 = ref[mm].topk(2).values
+            u = float(_ulp(t2[0]))
+            rows.append(dict(err=abs(float(scores[i][mm, tok]) - float(t2[0])) / u,
+                             margin=float(t2[0] - t2[1]) / u, agree=int(scores[i][mm].argmax()) == tok))
+    det = [r for r in rows if r["margin"] > 2 * LONG_BOUND_ULPS]
+    stats = dict(decisions=len(rows), agree=sum(r["agree"] for r in rows), determined=len(det),
+                 determined_agree=sum(r["agree"] for r in det), max_err_ulps=max(r["err"] for r in rows),
+                 mean_err_ulps=sum(r["err"] for r in rows) / len(rows), last_position=lc + p + len(trace))
+    if os.path.isdir("gpurun_out"):
+        json.dump(stats, open("gpurun_out/long_context.json", "w"), indent=1)
+    assert stats["decisions"] > 8000
+    assert stats["determined_agree"] == stats["determined"], stats
+    assert stats["max_err_ulps"] <= LONG_BOUND_ULPS, stats
+
+
+def test_kv_capacity_8_slots_5784_positions():
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    smax_req = 5784
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=smax_req, max_prefill=16, max_slots=8)
+    e = m.engine
+    assert e.smax >= smax_req
+    kv_bytes = (e.kc.numel() + e.vc.numel()) * e.kc.element_size()
+    assert kv_bytes == 2 * cfg.backbone.n_layer * 16 * 4 * e.smax * 128 * 2  # 16 rows = 8 CFG slot pairs
+    rows = 16
+    with torch.cuda.stream(e.stream):
+        e.row_pos[:rows] = torch.arange(5760, 5760 + rows, dtype=torch.int32, device=DEV)
+        e.row_kv[:rows] = torch.arange(rows, dtype=torch.int32, device=DEV)
+        e.x[:rows].normal_()
+        e.kc.normal_()
+        e.vc.normal_()
+    e.stream.synchronize()
+    e.step(1, use_graph=True, slots=8)
+    e.stream.synchronize()
+    e.check_errors()
+    assert torch.isfinite(e.logits[:rows]).all()
