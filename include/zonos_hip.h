@@ -79,6 +79,14 @@ int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, cons
 int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                   const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                   int ldo, float* part_o, float* part_lm, void* work, void* stream);
+/* Same op with an explicit kernel choice: 0 = library choice (as zmi_attention), 1 = the chunked
+ * kernel above (any length), 4 / 8 = the whole-query kernel with that many output-dim slices
+ * per (query, kv head): every slice reads all of the query's keys and no workgroup waits on
+ * another (max_pos < zmi_attention_max_keys_whole()). All variants return identical bits. */
+int zmi_attention_variant(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
+                          const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
+                          int ldo, float* part_o, float* part_lm, void* work, int variant, void* stream);
+int zmi_attention_max_keys_whole(void);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);

@@ -155,8 +155,9 @@ def test_gemv_qkv_rope_kv_write():
         assert kc[r, 0, :p].abs().sum() == 0 and vc[r, 0, :, :p].abs().sum() == 0
 
 
-def _attention(q, kc, vc, positions, kv_rows=None, hq=16, hkv=4):
-    """Run zmi_attention; kc [R][hkv][smax][hd], vc the same cache in the kernel's transposed layout."""
+def _attention(q, kc, vc, positions, kv_rows=None, hq=16, hkv=4, variant=0):
+    """Run zmi_attention_variant (0 = library choice); kc [R][hkv][smax][hd], vc the same cache in the
+    kernel's transposed layout."""
     L = _lib()
     hd, smax = kc.shape[-1], kc.shape[-2]
     n = len(positions)
@@ -169,9 +170,9 @@ def _attention(q, kc, vc, positions, kv_rows=None, hq=16, hkv=4):
     po = torch.zeros(nf, dtype=torch.float32, device=DEV)
     plm = torch.zeros(nf // hd * 2, dtype=torch.float32, device=DEV)
     for _ in range(2):  # the second launch checks that the hand-off state re-armed itself
-        L.check(L.lib().zmi_attention(q.data_ptr(), hq * hd, kc.data_ptr(), vt.data_ptr(), _lib().ptr(rk),
-                                      rp.data_ptr(), n, hq, hkv, hd, smax, smax - 1, out.data_ptr(), hq * hd,
-                                      po.data_ptr(), plm.data_ptr(), work.data_ptr(), stream_ptr()))
+        L.check(L.lib().zmi_attention_variant(q.data_ptr(), hq * hd, kc.data_ptr(), vt.data_ptr(), _lib().ptr(rk),
+                                              rp.data_ptr(), n, hq, hkv, hd, smax, smax - 1, out.data_ptr(), hq * hd,
+                                              po.data_ptr(), plm.data_ptr(), work.data_ptr(), variant, stream_ptr()))
         torch.cuda.synchronize()
         assert int(work[:4].view(torch.int32).item()) == 0, "cross-chunk hand-off timed out"
     return out
@@ -206,6 +207,29 @@ def test_attention_matches_reference_blocking(positions):
     q = rnd(R, H * hd, scale=2.0, seed=22)
     out = _attention(q, kc, vc, positions)
     _check_attention(out, q, kc, vc, positions)
+
+
+@pytest.mark.parametrize("hq,hkv", [(16, 4), (4, 1), (8, 4)])
+def test_attention_whole_query_variant_bit_identical_to_chunked(hq, hkv):
+    """The whole-query kernel (one workgroup per (query, kv head, dim slice), no cross-workgroup
+    exchange) restates the chunked kernel's arithmetic operation for operation: identical bits at
+    every position it covers, including chunk / block edges and the last covered position."""
+    hd = 128
+    lim = _lib().lib().zmi_attention_max_keys_whole()
+    smax = lim + 8
+    positions = [0, 1, 31, 32, 127, 128, 129, 300, 511, 512, 591, 640, 1023, 1024, 1030, lim - 2, lim - 1]
+    R = len(positions)
+    kc = rnd(R, hkv, smax, hd, seed=60)
+    vc = rnd(R, hkv, smax, hd, seed=61)
+    q = rnd(R, hq * hd, scale=3.0, seed=62)
+    ref = _attention(q, kc, vc, positions, hq=hq, hkv=hkv, variant=1)
+    # the whole-query kernel covers max_pos < lim: give it a cache view whose capacity is lim
+    for ds in (4, 8):
+        got = _attention(q, kc[:, :, :lim].contiguous(), vc[:, :, :lim].contiguous(), positions, hq=hq, hkv=hkv,
+                         variant=ds)
+        assert torch.equal(got, ref), (ds, (got != ref).nonzero()[:4].tolist())
+    _check_attention(got[[0, 6, 10, 14, R - 1]], q[[0, 6, 10, 14, R - 1]], kc[[0, 6, 10, 14, R - 1]],
+                     vc[[0, 6, 10, 14, R - 1]], [positions[i] for i in (0, 6, 10, 14, R - 1)], hq=hq, hkv=hkv)
 
 
 def test_attention_long_context_c5_positions():

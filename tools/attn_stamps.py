@@ -43,9 +43,9 @@ def run(pos_list, slots=1, reps=20):
         rel = []
         for _ in range(reps):
             st.zero_()
-            _lib.check(L.zmi_attention(q.data_ptr(), HQ * HD, kc.data_ptr(), vt.data_ptr(), None, rp.data_ptr(), rows,
-                                       HQ, HKV, HD, smax, smax - 1, out.data_ptr(), HQ * HD, po.data_ptr(),
-                                       plm.data_ptr(), work.data_ptr(), torch.cuda.current_stream().cuda_stream))
+            _lib.check(L.zmi_attention_variant(q.data_ptr(), HQ * HD, kc.data_ptr(), vt.data_ptr(), None, rp.data_ptr(),
+                                               rows, HQ, HKV, HD, smax, smax - 1, out.data_ptr(), HQ * HD, po.data_ptr(),
+                                               plm.data_ptr(), work.data_ptr(), 1, torch.cuda.current_stream().cuda_stream))
             torch.cuda.synchronize()
             s = st.cpu()
             live = s[:, 0] > 0

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--slots", type=int, default=1)
     ap.add_argument("--pos", type=int, default=591)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--attn-variants", default="0,1,4,8", help="zmi_attention_variant choices to time")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = zonos_v01_transformer()
@@ -66,8 +67,13 @@ def main():
         gbs = wbytes[name] / (us * 1e-6) / 1e9
         out[name] = dict(us=round(us, 2), weight_bytes=wbytes[name], GBps=round(gbs, 1), hbm_frac=round(gbs / 8000, 3))
     kv = rows * e.Hkv * e.hd * 2 * 2 * (args.pos + 1)
-    us = timed(lambda: [e._attention(i, e.q, rows, None, e.row_pos, e.smax - 1, e.attn) for i in range(L)], L)
-    out["attention"] = dict(us=round(us, 2), kv_bytes=kv, GBps=round(kv / (us * 1e-6) / 1e9, 1))
+    variants = [int(v) for v in args.attn_variants.split(",")]
+    for var in variants:
+        e.attn_variant = var
+        us = timed(lambda: [e._attention(i, e.q, rows, None, e.row_pos, e.smax - 1, e.attn) for i in range(L)], L)
+        key = "attention" if var == variants[0] else f"attention_v{var}"
+        out[key] = dict(us=round(us, 2), variant=var, kv_bytes=kv, GBps=round(kv / (us * 1e-6) / 1e9, 1))
+    e.attn_variant = variants[0]
     e.check_errors()
     for k, v in out.items():
         print(json.dumps(dict(kernel=k, slots=args.slots, pos=args.pos, **v)), flush=True)

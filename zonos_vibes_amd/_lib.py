@@ -69,6 +69,10 @@ _SIGS = {
                                    c_void_p]),
     "zmi_attention": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_attention_variant": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                      c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_void_p]),
+    "zmi_attention_max_keys_whole": (c_int, []),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_chunk": (c_int, []),

@@ -93,6 +93,7 @@ class HipEngine:
         self.stream = torch.cuda.Stream(self.dev)
         self.sptr = self.stream.cuda_stream
         self.w = None
+        self.attn_variant = 0  # zmi_attention_variant kernel choice (0 = library; all give identical bits)
         self._plans: dict[int, list] = {}
         self._graphs: dict[int, int] = {}
         self._alloc()
@@ -243,11 +244,11 @@ class HipEngine:
         return self._plans[rows]
 
     def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
-        _lib.check(self.lib.zmi_attention(q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(),
-                                          _lib.ptr(row_kv), row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd,
-                                          self.smax, max_pos, out.data_ptr(), self.H * self.hd,
-                                          self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(),
-                                          self.sptr), "attention")
+        _lib.check(self.lib.zmi_attention_variant(
+            q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(), _lib.ptr(row_kv),
+            row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd, self.smax, max_pos, out.data_ptr(), self.H * self.hd,
+            self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(), self.attn_variant, self.sptr),
+            "attention")
 
     def check_errors(self):
         """Raise if an attention launch gave up waiting on a cross-block hand-off (bounded spin)."""
