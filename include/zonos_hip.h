@@ -87,6 +87,19 @@ int zmi_attention_variant(const void* q, int ldq, const void* k_cache, const voi
                           const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                           int ldo, float* part_o, float* part_lm, void* work, int variant, void* stream);
 int zmi_attention_max_keys_whole(void);
+/* Fused decode block (reference _torch.py:114-136 for one decode step): the LayerNorm'd QKV
+ * projection `qkv` (EPI_QKV arguments as for zmi_gemv_launch: M <= 16 rows, K = 2048, 4 query heads
+ * per kv head, row_kv set) and the attention of every row at its position, in ONE launch whose
+ * attention workgroups load the cached K / V while the projection streams its weights. q, the KV
+ * cache writes and attn_out (bf16 [M][ldo]) are bit-identical to zmi_gemv_launch(QKV) followed by
+ * zmi_attention. gran: zmi_attn_block_gran_words(M, hkv) u64 words of {value, tag = position + 1}
+ * hand-off granules; a row's words must not hold tag pos + 1 from an earlier use when it runs at
+ * position pos (zero them when a row starts a new utterance; consecutive steps need nothing).
+ * err: set nonzero if a wait gave up. slices: 4 or 8 workgroups per (row, kv head).
+ * Positions < zmi_attention_max_keys_whole(). */
+int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                   void* stream);
+int64_t zmi_attn_block_gran_words(int rows, int hkv);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);

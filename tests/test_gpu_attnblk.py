@@ -1,0 +1,103 @@
+"""The fused decode block (zmi_attn_block: QKV projection + attention in ONE launch) against the
+same two ops as separate launches (zmi_gemv_launch EPI_QKV, then zmi_attention): q, the K / V
+cache writes and the attention output must be bit-identical, for any row count up to 16, mixed
+positions (chunk and 512-key block edges, position 0, the last covered position) and inactive rows.
+The separate path is itself pinned against the oracle / fp32 SDPA in test_gpu_kernels.py."""
+import ctypes
+
+import pytest
+import torch
+
+from tests.test_gpu_kernels import DEV, _check_attention, _lib, pack, rnd, stream_ptr
+
+pytestmark = pytest.mark.gpu
+
+D, H, HKV, HD = 2048, 16, 4, 128
+QKV_N = (H + 2 * HKV) * HD
+
+
+def _setup(positions, smax, seed):
+    from zonos_vibes_amd.engine import rope_table
+    R = len(positions)
+    W = rnd(QKV_N, D, scale=0.03, seed=seed)
+    X = rnd(R, D, scale=2.0, seed=seed + 1)
+    lw, lb = rnd(D, scale=0.1, seed=seed + 2) + 1, rnd(D, scale=0.02, seed=seed + 3)
+    kc = rnd(R, HKV, smax, HD, seed=seed + 4)
+    vt = rnd(R, HKV, HD, smax, seed=seed + 5)
+    return dict(W=pack(W), X=X, ln=(lw.contiguous(), lb.contiguous()), kc=kc, vt=vt, rope=rope_table(HD).to(DEV),
+                row_kv=torch.arange(R, dtype=torch.int32, device=DEV),
+                row_pos=torch.tensor(positions, dtype=torch.int32, device=DEV), smax=smax, R=R)
+
+
+def _args(st, q, kc, vt):
+    L = _lib()
+    (Wp, n_pad) = st["W"]
+    a = L.GemvArgs()
+    a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), st["X"].data_ptr(), st["R"], n_pad, D, D
+    a.ln_w, a.ln_b, a.eps = st["ln"][0].data_ptr(), st["ln"][1].data_ptr(), 1e-5
+    a.out, a.ldo, a.n_valid = q.data_ptr(), H * HD, QKV_N
+    a.row_kv, a.row_pos, a.k_cache, a.v_cache = st["row_kv"].data_ptr(), st["row_pos"].data_ptr(), kc.data_ptr(), \
+        vt.data_ptr()
+    a.smax, a.hq, a.hkv, a.hd, a.rope = st["smax"], H, HKV, HD, st["rope"].data_ptr()
+    return a
+
+
+def _separate(st):
+    L = _lib()
+    R, smax = st["R"], st["smax"]
+    q = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    kc, vt = st["kc"].clone(), st["vt"].clone()
+    a = _args(st, q, kc, vt)
+    L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), L.EPI_QKV, stream_ptr()), "gemv")
+    out = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    work = torch.zeros(L.lib().zmi_attention_work_bytes(R, H, HKV, HD, smax - 1), dtype=torch.uint8, device=DEV)
+    nf = L.lib().zmi_attention_partial_floats(R, H, HKV, HD, smax - 1)
+    po = torch.zeros(nf, dtype=torch.float32, device=DEV)
+    plm = torch.zeros(nf // HD * 2, dtype=torch.float32, device=DEV)
+    L.check(L.lib().zmi_attention_variant(q.data_ptr(), H * HD, kc.data_ptr(), vt.data_ptr(), None,
+                                          st["row_pos"].data_ptr(), R, H, HKV, HD, smax, smax - 1, out.data_ptr(),
+                                          H * HD, po.data_ptr(), plm.data_ptr(), work.data_ptr(), 1, stream_ptr()))
+    torch.cuda.synchronize()
+    return q, kc, vt, out
+
+
+def _fused(st, slices, reps=1):
+    L = _lib()
+    R = st["R"]
+    q = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    kc, vt = st["kc"].clone(), st["vt"].clone()
+    a = _args(st, q, kc, vt)
+    # hand-off granules hold stale tags of "earlier steps" (every tag except position + 1 of the row),
+    # as they do in a running decode
+    gran = torch.zeros(L.lib().zmi_attn_block_gran_words(R, HKV), dtype=torch.int64, device=DEV)
+    stale = torch.randint(0, 1 << 30, gran.shape, device=DEV)
+    gran.copy_(stale | ((torch.randint(1 << 20, 1 << 30, gran.shape, device=DEV)) << 32))
+    err = torch.zeros(4, dtype=torch.int32, device=DEV)
+    out = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    for _ in range(reps):  # a repeated launch at the same positions reads its own (equal) granules
+        L.check(L.lib().zmi_attn_block(ctypes.byref(a), gran.data_ptr(), err.data_ptr(), out.data_ptr(), H * HD,
+                                       slices, stream_ptr()), "attn_block")
+    torch.cuda.synchronize()
+    assert int(err[0].item()) == 0, "a wait for a hand-off gave up"
+    return q, kc, vt, out
+
+
+@pytest.mark.parametrize("positions", [
+    (591, 592),                                    # C2 mean position, one slot
+    (0, 1),                                        # the first key comes from this launch only
+    (127, 128, 511, 512, 1030, 1279),              # chunk / block edges and the last covered position
+    (5, -1, 300, 301, 63, 64, 700, -1, 1000, 1001, 31, 32, 255, 256, 900, 17),  # 16 rows, inactive rows
+])
+@pytest.mark.parametrize("slices", [4, 8])
+def test_attn_block_bit_identical_to_separate_launches(positions, slices):
+    st = _setup(positions, 1280, seed=70)
+    ref = _separate(st)
+    got = _fused(st, slices, reps=3)
+    live = [i for i, p in enumerate(positions) if p >= 0]
+    for name, r, g in zip(("q", "k_cache", "v_cache"), ref[:3], got[:3]):
+        assert torch.equal(r, g), name
+    assert torch.equal(ref[3][live], got[3][live]), "attention output"
+    # and the output is the reference attention of the projected q / K / V
+    pick = live[:3]
+    _check_attention(got[3][pick], got[0][pick], got[1][pick], got[2][pick].transpose(-1, -2).contiguous(),
+                     [positions[i] for i in pick])

@@ -90,6 +90,27 @@ def test_gemv_is_batch_invariant(K, ln):
         assert torch.equal(alt, ref)
 
 
+@pytest.mark.parametrize("K,M", [(2048, 2), (2048, 16), (2048, 37), (512, 5), (1024, 3)])
+def test_layernorm_rows_equals_gemv_prologue(K, M):
+    """zmi_layernorm_rows (norm_f of the backbone plugin) and the GEMV LayerNorm prologue share one
+    arithmetic (zmi_common.h): a plain GEMV of the normalised rows equals the LayerNorm'd GEMV."""
+    L = _lib()
+    N = 256
+    W, X = rnd(N, K, scale=0.05, seed=14), rnd(M, K, scale=3.0, seed=15)
+    lw, lb = (rnd(K, scale=0.2, seed=16) + 1).contiguous(), rnd(K, scale=0.05, seed=17)
+    xn = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    L.check(L.lib().zmi_layernorm_rows(X.data_ptr(), K, M, K, lw.data_ptr(), lb.data_ptr(), 1e-5, xn.data_ptr(), K,
+                                       stream_ptr()))
+    packed = pack(W)
+    a = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+    b = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+    gemv(W, X, L.EPI_F32, a, N, ln=(lw, lb), packed=packed)
+    gemv(W, xn, L.EPI_F32, b, N, packed=packed)
+    assert torch.equal(a, b)
+    ref = F.layer_norm(X.float().cpu(), (K,), lw.float().cpu(), lb.float().cpu(), 1e-5)
+    assert _ulp_close(xn, ref, 1) > 0.99
+
+
 def _ulp_close(a, b, ulps=1):
     a, b = a.float().cpu(), b.float().cpu()
     ulp = torch.ldexp(torch.ones_like(b), torch.frexp(b.abs().clamp_min(1e-30))[1] - 8)

@@ -29,6 +29,7 @@ def main():
     dev = torch.device("cuda", 0)
     m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=1040, max_prefill=16)
     e = m.engine
+    e.attn_block = False  # the unfused plan: QKV and attention as their own launches
     with torch.cuda.stream(e.stream):
         e.row_pos[:2] = args.pos
         e.x.normal_()

@@ -73,6 +73,8 @@ _SIGS = {
                                       c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                       c_void_p]),
     "zmi_attention_max_keys_whole": (c_int, []),
+    "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_chunk": (c_int, []),

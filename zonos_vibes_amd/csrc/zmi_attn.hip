@@ -31,6 +31,7 @@
 #include "zmi_common.h"
 #include "zmi_kernels.h"
 #include "zmi_attn_merge.h"
+#include "zmi_attn_ds.h"
 
 namespace {
 
@@ -38,42 +39,8 @@ using namespace zmi_attn;
 constexpr int NT = NWC * 64;
 constexpr unsigned SPIN_LIMIT = 1u << 20;
 
-struct AttnArgs {
-  const bf16_t* q;
-  int ldq;
-  const bf16_t* k;
-  const bf16_t* v;
-  const int* kv_row;
-  const int* pos;
-  int hkv, smax, nch;
-  float scale;
-  bf16_t* out;
-  int ldo;
-  unsigned* err;       // nonzero after a hand-off poll gave up
-  unsigned* tickets;   // [unit]
-  uint64_t* gran;      // [unit][nch][G]   {chunk max, tag}
-  float* part_o;       // [unit][nch][G][HD]
-  float* part_lm;      // [unit][nch][G][2]   l, M_j
-  unsigned long long* stamps;  // diagnostic build only
-};
 
-// Diagnostic build only (-DZMI_ATTN_STAMPS, tools/attn_stamps.py): thread 0 of every workgroup
-// writes s_memrealtime (100 MHz) at phase boundaries into a.stamps[block][8]; the real kernel has none.
-#ifdef ZMI_ATTN_STAMPS
-#define ZMI_ASTAMP(i)                                                                                    \
-  do {                                                                                                   \
-    if (threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
-  } while (0)
-#else
-#define ZMI_ASTAMP(i) \
-  do {                \
-  } while (0)
-#endif
 
-__device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                 0, 0, 0);
-}
 
 template <int G>
 __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
@@ -280,196 +247,10 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
   ZMI_ASTAMP(7);
 }
 
-// ---- Whole-query variant (decode at short and medium contexts) ------------------------------------
-// One workgroup of DNW waves per (query, kv head, slice of HD / DS output dims) covers EVERY key of
-// its query: all scores and softmax statistics (K is read by each of the DS slices of a unit; they
-// share one XCD under round-robin placement, so three of them read it from L2), and P.V for its own
-// dims only. No workgroup waits on another. The arithmetic is attn_kernel's operation for
-// operation, so both variants return identical bits and the launcher may pick either per launch:
-//   * scores per 32-key group: the same 4-MFMA chain over the same operand layout;
-//   * chunk maxima over CH keys; M_j over the chunks of blocks 0..j (max is exact);
-//   * per chunk and head: lane L takes keys L, L + 64 (e = 0 past the position), wave_sum -> l_c;
-//   * P.V per 32-key group from a zero accumulator, chunk o = group sums in group order (groups
-//     wholly past the position contribute +0 there, which is the identity: an MFMA from a +0
-//     accumulator never returns -0, so they are skipped here);
-//   * merge4's block recursion per (head, dim).
-// Keys up to DS_KEYS: a wave holds the K and V^T fragments of all its groups (DKM per wave) in
-// registers, all issued before the first MFMA.
-constexpr int DNW = 8;                    // waves per workgroup
-constexpr int DKM = 5;                    // 32-key groups per wave
-constexpr int DS_KEYS = 32 * DNW * DKM;   // 1280 keys (positions 0..1279)
-constexpr int DS_CH = DS_KEYS / CH;       // chunks
-constexpr int DS_BLK = (DS_KEYS + BLK - 1) / BLK;
-
 template <int G, int DS>
 __global__ __launch_bounds__(DNW * 64) void attn_ds_kernel(const AttnArgs a, int n_units) {
-  constexpr int CPG = CH / 32;     // 32-key groups per chunk (attn_kernel's waves)
-  constexpr int DT = 8 / DS;       // 16-dim MFMA column tiles per slice
-  constexpr int DSD = HD / DS;     // dims per slice
-  constexpr int NG = DNW * DKM;    // 32-key groups
-  __shared__ float sc[G][DS_KEYS];
-  __shared__ __attribute__((aligned(16))) bf16_t pb[G][DS_KEYS];
-  __shared__ float opart[NG][G][DSD];
-  __shared__ float mjc[DS_CH][G], ljc[DS_CH][G], mblk[DS_BLK][G];
-
-  // block -> (unit, slice): the DS slices of a unit take ids 8 apart (one XCD, speed only)
-  const int b = blockIdx.x, y = b >> 3;
-  const int s = y % DS, unit = 8 * (y / DS) + (b & 7);
-  if (unit >= n_units) return;
-  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
-  const int pos = a.pos[qi];
-  if (pos < 0) return;
-  const int nk = pos + 1, n32 = (nk + 31) >> 5, nc = pos / CH + 1;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int c16 = lane & 15, h4 = lane >> 4;
-  const int kvr = a.kv_row ? a.kv_row[qi] : qi;
-  const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
-
-  uint4 qf[4];
-  {
-    const bool real = c16 < G;
-    const bf16_t* qr = a.q + (size_t)qi * a.ldq + (kh * G + (real ? c16 : 0)) * HD + 8 * h4;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      qf[db] = *reinterpret_cast<const uint4*>(qr + 32 * db);
-      if (!real) qf[db] = uint4{0u, 0u, 0u, 0u};
-    }
-  }
-  // every K and V^T fragment of this wave's groups k = wave + DNW r, in flight at once
-  uint4 kf[DKM][2][4], vf[DKM][DT];
-#pragma unroll
-  for (int r = 0; r < DKM; ++r) {
-    const int k = wave + DNW * r;
-    if (k < n32) {
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const int key = min(32 * k + 16 * tt + c16, pos);
-        const bf16_t* kr = a.k + kvbase + (size_t)key * HD + 8 * h4;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) kf[r][tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
-      }
-      const int p0 = min(32 * k + 8 * h4, pos & ~7);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-        vf[r][dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * (DT * s + dt) + c16) * a.smax + p0);
-    }
-  }
-  // scores of every live key (keys past the position stay out of every max / sum below)
-#pragma unroll
-  for (int r = 0; r < DKM; ++r) {
-    const int k = wave + DNW * r;
-    if (k < n32) {
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        f32x4_t sv = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int db = 0; db < 4; ++db) sv = mfma16(qf[db], kf[r][tt][db], sv);
-        const int key = 32 * k + 16 * tt + c16;
-        if (h4 == 0) {
-#pragma unroll
-          for (int i = 0; i < G; ++i) sc[i][key] = sv[i] * a.scale;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // chunk maxima (task = chunk x head)
-  for (int task = wave; task < nc * G; task += DNW) {
-    const int c = task / G, g = task - c * G;
-    float m = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < CH / 64; ++i) {
-      const int key = c * CH + lane + 64 * i;
-      m = fmaxf(m, key < nk ? sc[g][key] : -INFINITY);
-    }
-    m = wave_max(m);
-    if (lane == 0) mjc[c][g] = m;
-  }
-  __syncthreads();
-  const int nb = (nc + CPB - 1) / CPB;
-  if (t < nb * G) {  // M_j = max over the chunks of blocks 0..j
-    const int j = t / G, g = t - j * G, dep = min((j + 1) * CPB, nc);
-    float m = -INFINITY;
-    for (int c = 0; c < dep; ++c) m = fmaxf(m, mjc[c][g]);
-    mblk[j][g] = m;
-  }
-  __syncthreads();
-  // e = exp(s - M_j), l per chunk (attn_kernel's lane order and wave_sum), P = bf16(e)
-  for (int task = wave; task < nc * G; task += DNW) {
-    const int c = task / G, g = task - c * G;
-    const float M = mblk[c / CPB][g];
-    float l = 0.f;
-#pragma unroll
-    for (int i = 0; i < CH / 64; ++i) {
-      const int key = c * CH + lane + 64 * i;
-      const float e = key < nk ? expf(sc[g][key] - M) : 0.f;
-      l += e;
-      pb[g][key] = (bf16_t)f2bf(e);
-    }
-    l = wave_sum(l);
-    if (lane == 0) ljc[c][g] = l;
-  }
-  __syncthreads();
-  // P.V of this slice's dims, per live group
-#pragma unroll
-  for (int r = 0; r < DKM; ++r) {
-    const int k = wave + DNW * r;
-    if (k < n32) {
-      uint4 pf = uint4{0u, 0u, 0u, 0u};
-      if (c16 < G) pf = *reinterpret_cast<const uint4*>(&pb[c16][32 * k + 8 * h4]);
-      const int kbase = 32 * k + 8 * h4;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        uint4 v = vf[r][dt];
-        if (kbase + 8 > nk) {
-          uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint32_t lo = kbase + 2 * e < nk ? 0x0000ffffu : 0u;
-            const uint32_t hi = kbase + 2 * e + 1 < nk ? 0xffff0000u : 0u;
-            w[e] &= lo | hi;
-          }
-          v = uint4{w[0], w[1], w[2], w[3]};
-        }
-        const f32x4_t o = mfma16(pf, v, f32x4_t{0.f, 0.f, 0.f, 0.f});
-        if (h4 == 0) {
-#pragma unroll
-          for (int i = 0; i < G; ++i) opart[k][i][16 * dt + c16] = o[i];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // chunk sums and merge4's block recursion, one thread per (head, dim of the slice)
-  if (t < G * DSD) {
-    const int g = t / DSD, dl = t - g * DSD;
-    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
-    for (int c = 0; c < nc; ++c) {
-      float oc = opart[CPG * c][g][dl];
-      for (int w = 1; w < CPG && CPG * c + w < n32; ++w) oc += opart[CPG * c + w][g][dl];
-      if (c % CPB == 0) {
-        ob = oc;
-        lb = ljc[c][g];
-        mb = mblk[c / CPB][g];
-      } else {
-        ob += oc;
-        lb += ljc[c][g];
-      }
-      if (c % CPB == CPB - 1 || c == nc - 1) {
-        if (c < CPB) {
-          acc = ob;
-          l = lb;
-        } else {
-          const float et = expf(mprev - mb);
-          l = lb + et * l;
-          acc = acc * et + ob;
-        }
-        mprev = mb;
-      }
-    }
-    const float rl = 1.0f / l;
-    a.out[(size_t)qi * a.ldo + (kh * G + g) * HD + DSD * s + dl] = (bf16_t)f2bf(acc * rl);
-  }
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  ds_body<G, DS>(a, n_units, blockIdx.x, smem);
 }
 
 struct WorkLayout {
@@ -507,8 +288,12 @@ template <int G>
 hipError_t launch_ds(const AttnArgs& a, int n_units, int ds, hipStream_t s) {
   const unsigned blocks = (unsigned)((n_units + 7) / 8) * 8 * ds;
   switch (ds) {
-    case 4: hipLaunchKernelGGL((attn_ds_kernel<G, 4>), dim3(blocks), dim3(DNW * 64), 0, s, a, n_units); break;
-    case 8: hipLaunchKernelGGL((attn_ds_kernel<G, 8>), dim3(blocks), dim3(DNW * 64), 0, s, a, n_units); break;
+    case 4:
+      hipLaunchKernelGGL((attn_ds_kernel<G, 4>), dim3(blocks), dim3(DNW * 64), (DsImg<G, 4>::BYTES), s, a, n_units);
+      break;
+    case 8:
+      hipLaunchKernelGGL((attn_ds_kernel<G, 8>), dim3(blocks), dim3(DNW * 64), (DsImg<G, 8>::BYTES), s, a, n_units);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -559,9 +344,14 @@ extern "C" int zmi_attention_variant(const void* q, int ldq, const void* k_cache
   a.stamps = (unsigned long long*)(wb + w.stamps);
   hipStream_t s = (hipStream_t)stream;
   // variant: 0 = library choice, 1 = chunked (any length), 4 / 8 = whole-query kernel with that
-  // many dim slices (max_pos < DS_KEYS). Both give identical bits; the choice is speed only.
-  if (variant == 0) variant = (max_pos < DS_KEYS) ? 4 : 1;
+  // many dim slices (max_pos < DS_KEYS). Both give identical bits; the choice is speed only. As its
+  // own launch the whole-query kernel is bound by one CU's ~40 GB/s of K reads (C2 decode: 8.3 /
+  // 10.1 / 15.1 us at positions 300 / 591 / 1000 against 10.4 / 10.6 / 10.8 chunked), so the
+  // library picks the chunked kernel; the whole-query form pays off where its K/V loads overlap
+  // the QKV projection (zmi_attn_block).
+  if (variant == 0) variant = 1;
   if (variant != 1) {
+    a.stamps = nullptr;  // the diagnostic stamp area is laid out for the chunked grid
     if (max_pos >= DS_KEYS) return zmi_fail_msg("attention: the whole-query variant covers positions < 1280");
     if ((int64_t)n_query * hkv * variant > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
     const int n_units = n_query * hkv;

@@ -1,0 +1,507 @@
+// Fused QKV projection + decode attention: ONE launch for reference zonos/backbone/_torch.py:114-136
+// (norm -> in_proj -> rotary -> KV-cache update -> scaled_dot_product_attention) of a decode step.
+//
+// Why: as separate launches the attention paid a kernel boundary plus its own K / V load latency,
+// ~12 us per layer at C2 against ~6 us for the projection before it. One CU moves only ~64 KB at a
+// time (~20-40 GB/s), so a query's 300 KB of K / V (position 591) must be spread over several CUs,
+// and those CUs must then combine results. Here the attention workgroups are extra workgroups of the
+// projection's launch: they load their share of the cached K / V (positions < pos, written by
+// earlier launches) at launch start, under the projection's weight stream, and the hand-offs are
+// 8-byte {value, tag} granules (cdna_hip_programming.md §6 Guideline 16 R2: the data is its own
+// flag; tag = position + 1, so consecutive steps never mistake each other's granules and nothing is
+// re-armed; a row that starts a new utterance has its granules zeroed by the engine):
+//   1. projection -> attention: every bf16 pair of q and of the new K / V row (zmi_gemv_impl.h);
+//   2. attention -> attention: each of the S workgroups of a (query, kv head) computes the scores of
+//      every S-th 32-key group and publishes them; every workgroup gathers all scores, then runs the
+//      softmax and P.V for its own HD / S output dims (zmi_attn_ds.h ds_tail).
+// Roles by block index (dispatch runs in index order, so a waiting attention workgroup never holds
+// a slot a projection workgroup still needs; every spin is bounded and reports to `err`):
+//   [0, n_qkv)           gemv_body (zmi_gemv_impl.h): LayerNorm prologue, the QKV projection for 16
+//                        columns, epilogue RoPE + KV-cache write + granules;
+//   [n_qkv, +units x S)  xs_body below.
+// The arithmetic is the separate kernels' operation for operation (bit-identical outputs, tested);
+// both roles run 512-thread workgroups: the projection with G = 2 groups x W = 4 waves, the K = 2048
+// shape every launch form uses.
+#include <algorithm>
+
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+#include "zmi_gemv_impl.h"
+#include "zmi_attn_ds.h"
+
+namespace {
+
+using namespace zmi_attn;
+constexpr int QG = 2, QW = 4, QNL = 8, QRT = 16;  // the projection role's gemv_body shape
+static_assert(QG * QW == DNW, "both roles run the same block size");
+constexpr int XG = 4;                         // query heads per kv head
+constexpr int QKV_GRAN = (XG + 2) * HD / 2;   // q pairs | k pairs | v pairs per (row, kv head)
+constexpr int GRAN_STRIDE = QKV_GRAN + XG * DS_KEYS;  // + the score granules [XG][DS_KEYS]
+constexpr int NT = DNW * 64;
+constexpr unsigned XS_SPIN = 1u << 16;
+
+__device__ __forceinline__ uint32_t tag_of(uint64_t g) { return (uint32_t)(g >> 32); }
+
+__device__ __forceinline__ void give_up(const AttnArgs& a) {
+  __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 of an attention workgroup only receives the projection's granules (it issues no K / V
+// loads, so its polls are not queued behind them); waves 1..7 ("workers") hold the K / V fragments.
+// Worker ww owns the 128-key chunks c = ww + XNWK rc: the V^T fragments of their four 32-key groups
+// (its P.V sums a chunk's groups in group order in registers: the chunked kernel's chunk sum).
+constexpr int XNWK = DNW - 1;                         // worker waves
+constexpr int XCH = DS_KEYS / CH;                     // chunks
+constexpr int XRC = (XCH + XNWK - 1) / XNWK;          // chunks per worker
+constexpr int CPG = CH / 32;                          // 32-key groups per chunk
+constexpr int XKPT = (DS_KEYS + NT - 1) / NT;         // keys per thread in the score gather
+
+template <int S>
+struct XsImg {
+  static constexpr int DSD = HD / S;
+  static constexpr size_t SC = 0;                                   // float [XG][DS_KEYS] scores
+  static constexpr size_t PB = SC + (size_t)XG * DS_KEYS * 4;       // bf16  [XG][DS_KEYS] P
+  static constexpr size_t OC = PB + (size_t)XG * DS_KEYS * 2;       // float [XCH][XG][DSD] chunk P.V
+  static constexpr size_t MJ = OC + (size_t)XCH * XG * DSD * 4;     // float [XCH][XG] chunk maxima
+  static constexpr size_t LJ = MJ + (size_t)XCH * XG * 4;           // float [XCH][XG] chunk exp sums
+  static constexpr size_t MB = LJ + (size_t)XCH * XG * 4;           // float [DS_BLK][XG] M_j
+  static constexpr size_t QKV = MB + (size_t)DS_BLK * XG * 4;       // u32 [QKV_GRAN] q | k | v pairs of pos
+  static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
+};
+
+template <int S>
+__device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
+  constexpr int OWN = (DS_KEYS / 32 + S - 1) / S;       // score groups of one workgroup
+  constexpr int KPW = (OWN + XNWK - 1) / XNWK;          // score groups per worker wave
+  constexpr int DT = 8 / S;
+  using I = XsImg<S>;
+  constexpr int DSD = I::DSD;
+  float(&sc)[XG][DS_KEYS] = *reinterpret_cast<float(*)[XG][DS_KEYS]>(smem + I::SC);
+  bf16_t(&pb)[XG][DS_KEYS] = *reinterpret_cast<bf16_t(*)[XG][DS_KEYS]>(smem + I::PB);
+  float(&ocs)[XCH][XG][DSD] = *reinterpret_cast<float(*)[XCH][XG][DSD]>(smem + I::OC);
+  float(&mjc)[XCH][XG] = *reinterpret_cast<float(*)[XCH][XG]>(smem + I::MJ);
+  float(&ljc)[XCH][XG] = *reinterpret_cast<float(*)[XCH][XG]>(smem + I::LJ);
+  float(&mblk)[DS_BLK][XG] = *reinterpret_cast<float(*)[DS_BLK][XG]>(smem + I::MB);
+  uint32_t* qkv_lds = reinterpret_cast<uint32_t*>(smem + I::QKV);
+
+  const int y = b >> 3;
+  const int s = y % S, unit = 8 * (y / S) + (b & 7);
+  if (unit >= n_units) return;
+  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
+  const int pos = a.pos[qi];
+  if (pos < 0) return;
+  ZMI_ASTAMP(0);
+  const uint32_t tag = (uint32_t)pos + 1u;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, ww = wave - 1;
+  const int c16 = lane & 15, h4 = lane >> 4;
+  const int kvr = a.kv_row ? a.kv_row[qi] : qi;
+  const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
+  const int nk = pos + 1, n32 = (pos + 32) >> 5, nc = pos / CH + 1;
+  uint64_t* gu = gran + (size_t)unit * GRAN_STRIDE;  // unit = query row x hkv + kv head, as the producers index
+  uint64_t* gs = gu + QKV_GRAN;
+
+  // (1) workers: the cached K rows of the workgroup's score groups k = s + S (ww + XNWK j) and the
+  // V^T fragments of their chunks' groups (dim slice s): positions < pos only
+  const int pc = max(pos - 1, 0);
+  uint4 kf[KPW][2][4], vf[XRC][CPG][DT];
+  if (wave > 0) {
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      const int k = s + S * (ww + XNWK * j);
+      if (ww + XNWK * j < OWN && k < n32) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const bf16_t* kr = a.k + kvbase + (size_t)min(32 * k + 16 * tt + c16, pc) * HD + 8 * h4;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) kf[j][tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
+        }
+      }
+    }
+#pragma unroll
+    for (int rc = 0; rc < XRC; ++rc)
+#pragma unroll
+      for (int q4 = 0; q4 < CPG; ++q4) {
+        const int k = CPG * (ww + XNWK * rc) + q4;
+        if (k < n32) {
+          const int p0 = min(32 * k + 8 * h4, pos & ~7);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+            vf[rc][q4][dt] =
+                *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * (DT * s + dt) + c16) * a.smax + p0);
+        }
+      }
+  } else {
+    // (2) wave 0: this position's q, K row and V row (QKV_GRAN pairs; 6 per lane), polled with two
+    // sweeps in flight a fraction of a round trip apart, then staged in LDS for the workers
+    uint64_t A[6], B[6];
+    auto sweep = [&](uint64_t(&g)[6]) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) g[i] = ld_wt64(gu + lane + 64 * i);
+    };
+    auto ready = [&](const uint64_t(&g)[6]) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) ok = ok && tag_of(g[i]) == tag;
+      return __all(ok);
+    };
+    auto stage = [&](const uint64_t(&g)[6]) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) qkv_lds[lane + 64 * i] = (uint32_t)g[i];
+    };
+    sweep(A);
+    __builtin_amdgcn_s_sleep(8);
+    sweep(B);
+    for (unsigned spins = 0;; spins += 2) {
+      if (ready(A)) {
+        stage(A);
+        break;
+      }
+      sweep(A);
+      __builtin_amdgcn_s_sleep(8);
+      if (ready(B)) {
+        stage(B);
+        break;
+      }
+      sweep(B);
+      __builtin_amdgcn_s_sleep(8);
+      if (spins > XS_SPIN) {
+        give_up(a);
+        stage(A);
+        break;
+      }
+    }
+    ZMI_ASTAMP(1);
+  }
+  __syncthreads();
+  uint4 qf[4];
+  if (wave > 0) {
+    const uint4* q4p = reinterpret_cast<const uint4*>(qkv_lds);
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+      qf[db] = c16 < XG ? q4p[(c16 * HD + 8 * h4 + 32 * db) >> 3] : uint4{0u, 0u, 0u, 0u};
+    // the K row of pos replaces the fragment of the lane whose key it is; the V^T slot of pos is
+    // patched in the fragment whose 8 positions hold it
+#pragma unroll
+    for (int j = 0; j < KPW; ++j)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+        if (ww + XNWK * j < OWN && 32 * (s + S * (ww + XNWK * j)) + 16 * tt + c16 == pos) {
+#pragma unroll
+          for (int db = 0; db < 4; ++db) kf[j][tt][db] = q4p[(XG * HD + 8 * h4 + 32 * db) >> 3];
+        }
+#pragma unroll
+    for (int rc = 0; rc < XRC; ++rc)
+#pragma unroll
+      for (int q4 = 0; q4 < CPG; ++q4) {
+        const int kb = 32 * (CPG * (ww + XNWK * rc) + q4) + 8 * h4;
+        if (kb <= pos && pos < kb + 8) {
+          const int sl = pos - kb, wi = sl >> 1, sh = (sl & 1) * 16;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const int d = 16 * (DT * s + dt) + c16;
+            const uint32_t pr = qkv_lds[(XG + 1) * HD / 2 + (d >> 1)];
+            const uint32_t val = (d & 1) ? (pr >> 16) : (pr & 0xffffu);
+            uint32_t w[4] = {vf[rc][q4][dt].x, vf[rc][q4][dt].y, vf[rc][q4][dt].z, vf[rc][q4][dt].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (e == wi) w[e] = (w[e] & ~(0xffffu << sh)) | (val << sh);
+            vf[rc][q4][dt] = uint4{w[0], w[1], w[2], w[3]};
+          }
+        }
+      }
+  }
+
+  // (3) scores of this workgroup's groups (the chunked kernel's MFMA chain): into LDS and out as
+  // granules for the other S - 1 workgroups of the query
+#pragma unroll
+  for (int j = 0; j < KPW; ++j) {
+    const int k = s + S * (ww + XNWK * j);
+    if (wave > 0 && ww + XNWK * j < OWN && k < n32) {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        f32x4_t sv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int db = 0; db < 4; ++db) sv = mfma16(qf[db], kf[j][tt][db], sv);
+        const int key = 32 * k + 16 * tt + c16;
+        if (h4 == 0 && key <= pos) {
+#pragma unroll
+          for (int i = 0; i < XG; ++i) {
+            const float v = sv[i] * a.scale;
+            sc[i][key] = v;
+            st_wt64(gs + (size_t)i * DS_KEYS + key, (uint64_t)__float_as_uint(v) | ((uint64_t)tag << 32));
+          }
+        }
+      }
+    }
+  }
+
+  // (4) gather the other workgroups' scores: thread t takes keys t + NT i (all heads), two sweeps
+  // in flight; a key's four granules are kept once all carry the tag
+  {
+    unsigned pend = 0;
+#pragma unroll
+    for (int i = 0; i < XKPT; ++i) {
+      const int key = t + NT * i;
+      if (key < nk && (key >> 5) % S != s) pend |= 1u << i;
+    }
+    uint64_t A[XKPT][XG], B[XKPT][XG];
+    auto sweep = [&](uint64_t(&g)[XKPT][XG]) {
+#pragma unroll
+      for (int i = 0; i < XKPT; ++i)
+#pragma unroll
+        for (int h = 0; h < XG; ++h) g[i][h] = ((pend >> i) & 1) ? ld_wt64(gs + h * DS_KEYS + t + NT * i) : 0ull;
+    };
+    auto take = [&](const uint64_t(&g)[XKPT][XG]) {
+#pragma unroll
+      for (int i = 0; i < XKPT; ++i) {
+        bool ok = (pend >> i) & 1;
+#pragma unroll
+        for (int h = 0; h < XG; ++h) ok = ok && tag_of(g[i][h]) == tag;
+        if (ok) {
+#pragma unroll
+          for (int h = 0; h < XG; ++h) sc[h][t + NT * i] = __uint_as_float((uint32_t)g[i][h]);
+          pend &= ~(1u << i);
+        }
+      }
+    };
+    if (pend) {
+      sweep(A);
+      __builtin_amdgcn_s_sleep(6);
+      sweep(B);
+    }
+    for (unsigned spins = 0; pend; spins += 2) {
+      take(A);
+      if (!pend) break;
+      sweep(A);
+      __builtin_amdgcn_s_sleep(6);
+      take(B);
+      if (!pend) break;
+      sweep(B);
+      __builtin_amdgcn_s_sleep(6);
+      if (spins > XS_SPIN) {
+        give_up(a);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(2);
+
+  // (5) softmax statistics: tasks (chunk, head), wave + DNW i of them per wave, interleaved
+  constexpr int NTASK = (XCH * XG + DNW - 1) / DNW;
+  const int ntask = nc * XG;
+  {  // chunk maxima
+    float m[NTASK];
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) {
+      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
+      m[i] = -INFINITY;
+      if (task < ntask) {
+#pragma unroll
+        for (int ii = 0; ii < CH / 64; ++ii) {
+          const int key = c * CH + lane + 64 * ii;
+          m[i] = fmaxf(m[i], key < nk ? sc[g][key] : -INFINITY);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) m[i] = wave_max(m[i]);
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) {
+      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
+      if (task < ntask && lane == 0) mjc[c][g] = m[i];
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(3);
+  {  // M_j = max over the chunks of blocks 0..j; e = exp(s - M_j), l per chunk, P = bf16(e)
+    float l[NTASK];
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) {
+      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
+      l[i] = 0.f;
+      if (task < ntask) {
+        const int j = c / CPB, dep = min((j + 1) * CPB, nc);
+        const float M = wave_max(lane < dep ? mjc[lane][g] : -INFINITY);  // exact: max is order-free
+        if (c % CPB == 0 && lane == 0) mblk[j][g] = M;
+#pragma unroll
+        for (int ii = 0; ii < CH / 64; ++ii) {
+          const int key = c * CH + lane + 64 * ii;
+          const float e = key < nk ? expf(sc[g][key] - M) : 0.f;
+          l[i] += e;
+          pb[g][key] = (bf16_t)f2bf(e);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) l[i] = wave_sum(l[i]);
+#pragma unroll
+    for (int i = 0; i < NTASK; ++i) {
+      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
+      if (task < ntask && lane == 0) ljc[c][g] = l[i];
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(4);
+  // (6) workers: P.V of the slice's dims, each chunk's groups summed in group order in registers
+  if (wave > 0) {
+#pragma unroll
+    for (int rc = 0; rc < XRC; ++rc) {
+      const int c = ww + XNWK * rc;
+      if (c < nc) {
+        f32x4_t oc[DT];
+#pragma unroll
+        for (int q4 = 0; q4 < CPG; ++q4) {
+          const int k = CPG * c + q4;
+          if (k < n32) {
+            uint4 pf = uint4{0u, 0u, 0u, 0u};
+            if (c16 < XG) pf = *reinterpret_cast<const uint4*>(&pb[c16][32 * k + 8 * h4]);
+            const int kbase = 32 * k + 8 * h4;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) {
+              uint4 v = vf[rc][q4][dt];
+              if (kbase + 8 > nk) {
+                uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const uint32_t lo = kbase + 2 * e < nk ? 0x0000ffffu : 0u;
+                  const uint32_t hi = kbase + 2 * e + 1 < nk ? 0xffff0000u : 0u;
+                  w[e] &= lo | hi;
+                }
+                v = uint4{w[0], w[1], w[2], w[3]};
+              }
+              const f32x4_t o = mfma16(pf, v, f32x4_t{0.f, 0.f, 0.f, 0.f});
+              if (q4 == 0) {
+                oc[dt] = o;
+              } else {
+                oc[dt][0] += o[0];
+                oc[dt][1] += o[1];
+                oc[dt][2] += o[2];
+                oc[dt][3] += o[3];
+              }
+            }
+          }
+        }
+        if (h4 == 0) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int i = 0; i < XG; ++i) ocs[c][i][16 * dt + c16] = oc[dt][i];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(5);
+  // (7) the block recursion (zmi_attn_merge.h), one thread per (head, dim of the slice)
+  if (t < XG * DSD) {
+    const int g = t / DSD, dl = t - g * DSD;
+    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float oc = ocs[c][g][dl];
+      if (c % CPB == 0) {
+        ob = oc;
+        lb = ljc[c][g];
+        mb = mblk[c / CPB][g];
+      } else {
+        ob += oc;
+        lb += ljc[c][g];
+      }
+      if (c % CPB == CPB - 1 || c == nc - 1) {
+        if (c < CPB) {
+          acc = ob;
+          l = lb;
+        } else {
+          const float et = expf(mprev - mb);
+          l = lb + et * l;
+          acc = acc * et + ob;
+        }
+        mprev = mb;
+      }
+    }
+    const float rl = 1.0f / l;
+    a.out[(size_t)qi * a.ldo + (kh * XG + g) * HD + DSD * s + dl] = (bf16_t)f2bf(acc * rl);
+  }
+  ZMI_ASTAMP(6);
+}
+
+template <int S>
+__global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
+                                                        int n_units, uint64_t* gran) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  if (b < n_qkv)
+    zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_LN, ZMI_EPI_QKV, 1, 1>(
+        qa, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, GRAN_STRIDE});
+  else
+    xs_body<S>(at, n_units, b - n_qkv, smem, gran);
+}
+
+template <int S>
+hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArgs& at, int n_units, uint64_t* gran,
+                        hipStream_t s) {
+  // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
+  // instead of sharing a CU's ~64 KB of loads in flight
+  const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, true), XsImg<S>::BYTES,
+                               zmi_gemv::LDS_MAX / 2 + 1024});
+  if (lds > zmi_gemv::LDS_MAX) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)zmi_gemv::LDS_MAX);
+    if (attr != hipSuccess) return attr;
+  }
+  const int n_xs = (n_units + 7) / 8 * 8 * S;
+  hipLaunchKernelGGL(attn_block_kernel<S>, dim3((unsigned)(n_qkv + n_xs)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
+                     n_units, gran);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int64_t zmi_attn_block_gran_words(int rows, int hkv) {
+  return (rows <= 0 || hkv <= 0) ? -1 : (int64_t)rows * hkv * GRAN_STRIDE;
+}
+
+extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                              void* stream) {
+  const ZmiGemvArgs& a = *qkv;
+  if (a.K != 2048 || !a.ln_w) return zmi_fail_msg("attn_block: the QKV projection must be LayerNorm'd with K = 2048");
+  if (a.M < 1 || a.M > QRT) return zmi_fail_msg("attn_block: 1 <= M <= 16 rows (one row tile)");
+  if (a.hd != HD || a.hkv <= 0 || a.hq != XG * a.hkv)
+    return zmi_fail_msg("attn_block: head_dim 128, 4 query heads per kv head");
+  if (a.N != (a.hq + 2 * a.hkv) * a.hd || a.n_valid != a.N) return zmi_fail_msg("attn_block: N = (hq + 2 hkv) hd");
+  if (a.smax - 1 >= DS_KEYS) return zmi_fail_msg("attn_block: positions must stay below zmi_attention_max_keys_whole()");
+  if (a.smax % 8 || !a.row_pos || !a.row_kv || !a.rope || !a.k_cache || !a.v_cache || !gran || !err || !attn_out)
+    return zmi_fail_msg("attn_block: missing buffers (or smax % 8)");
+  if (ldo % 8 || a.ldx % 8) return zmi_fail_msg("attn_block: ldo / ldx must be multiples of 8");
+  const int n_cb = a.N / 8 / QG;
+  const int n_qkv = (n_cb + 7) / 8 * 8;
+  const int n_units = a.M * a.hkv;
+
+  AttnArgs at{};
+  at.q = (const bf16_t*)a.out;
+  at.ldq = a.ldo;
+  at.k = (const bf16_t*)a.k_cache;
+  at.v = (const bf16_t*)a.v_cache;
+  at.kv_row = a.row_kv;
+  at.pos = a.row_pos;
+  at.hkv = a.hkv;
+  at.smax = a.smax;
+  at.scale = 1.0f / sqrtf((float)HD);
+  at.out = (bf16_t*)attn_out;
+  at.ldo = ldo;
+  at.err = err;
+  // diagnostic builds (-DZMI_ATTN_STAMPS -DZMI_GEMV_STAMPS): both roles stamp into qkv->diag, indexed
+  // by block (tools/attnblk_stamps.py)
+  at.stamps = a.diag ? reinterpret_cast<unsigned long long*>(a.diag) + (size_t)a.reserved * 4096 * 8 : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (slices) {
+    case 4: e = launch_block<4>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, s); break;
+    case 8: e = launch_block<8>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, s); break;
+    default: return zmi_fail_msg("attn_block: slices must be 4 or 8");
+  }
+  ZMI_CHECK(e);
+  return 0;
+}

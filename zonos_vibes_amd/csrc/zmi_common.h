@@ -77,6 +77,45 @@ __device__ __forceinline__ float wave_max(float v) {
   return fmaxf(fmaxf(lane_read(v, 0), lane_read(v, 16)), fmaxf(lane_read(v, 32), lane_read(v, 48)));
 }
 
+// ---- LayerNorm row arithmetic (nn.LayerNorm, reference _torch.py:62,88,90), shared by the GEMV
+// prologue (zmi_gemv_impl.h) and zmi_layernorm_rows so both give the same bits. A row of K elements
+// is cut into ln_parts(K) contiguous parts, each reduced by one wave: lane L owns the 8-element
+// chunks at q K / NQ + 8 (L + 64 i), i < K / (512 NQ); fp32 sums in chunk order, DPP wave sum per
+// part, parts combined as (p0 + p1) + (p2 + p3). Two passes (mean, then squared deviations).
+__host__ __device__ constexpr int ln_parts(int K) { return K >= 2048 ? 4 : (K >= 1024 ? 2 : 1); }
+__device__ __forceinline__ float ln_chunk_sum(const uint4& xv, float mean, bool sq) {
+  const uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
+  float t = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (sq) {
+      const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
+      t += d0 * d0 + d1 * d1;
+    } else {
+      t += bf2f(u[j]) + bf2f(u[j] >> 16);
+    }
+  }
+  return t;
+}
+template <int NQ>
+__device__ __forceinline__ float ln_combine(const float* p) {
+  if (NQ == 4) return (p[0] + p[1]) + (p[2] + p[3]);
+  if (NQ == 2) return p[0] + p[1];
+  return p[0];
+}
+// y = bf16((x * rstd - mean * rstd) * w + b) on one 8-element chunk
+__device__ __forceinline__ uint4 ln_apply(const uint4& xv, const uint4& gw, const uint4& gb, float rstd, float nbias) {
+  uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
+  const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float y0 = (bf2f(u[j]) * rstd + nbias) * bf2f(uw[j]) + bf2f(ub[j]);
+    const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
+    u[j] = f2bf(y0) | (f2bf(y1) << 16);
+  }
+  return uint4{u[0], u[1], u[2], u[3]};
+}
+
 // splitmix64 finaliser (shared with zonos_vibes_amd/synthetic.py)
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

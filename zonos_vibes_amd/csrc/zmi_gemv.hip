@@ -51,8 +51,8 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
     return zmi_fail_msg("gemv: K must be 512, 1024, 2048, 4096 or 8192");
   if (a.M < 1) return zmi_fail_msg("gemv: M must be >= 1");
   if (a.ldx % 8) return zmi_fail_msg("gemv: ldx must be a multiple of 8 (16-byte rows)");
-  if (a.groups < 0 || a.groups > 2 || (a.groups == 2 && !(sh.W == 2 && sh.NL == 16)))
-    return zmi_fail_msg("gemv: groups must be 0 (library choice), 1, or 2 for the LayerNorm'd K = 2048 shape");
+  if (a.groups < 0 || a.groups > 2 || (a.groups == 2 && a.K != 2048))
+    return zmi_fail_msg("gemv: groups must be 0 (library choice), 1, or 2 for K = 2048");
   if (epi == ZMI_EPI_QKV && (a.hd % 8 || a.smax <= 0 || !a.row_pos || !a.row_kv || !a.rope))
     return zmi_fail_msg("gemv: the QKV epilogue needs row_pos, row_kv, rope, smax and hd % 8 == 0");
   hipStream_t s = (hipStream_t)stream;

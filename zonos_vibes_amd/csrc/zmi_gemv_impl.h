@@ -79,17 +79,28 @@ struct Img {
   } while (0)
 #endif
 
-template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
-__global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt) {
+// In-launch hand-off of the QKV projection to the attention workgroups of zmi_attn_block
+// (zmi_attnblk.hip): every bf16 pair of q and of this step's K / V rows is ALSO stored as an 8-byte
+// {pair, tag = position + 1} granule (one sc1 store: the data is its own flag, cdna_hip_programming.md
+// §6 Guideline 16 R2), so the consumer needs no counter and nothing is re-armed.
+// Per query row and kv head the granule area holds QKV_GRAN words: q of the G heads (G HD / 2 pairs),
+// then k (HD / 2) and v (HD / 2); the score granules follow (zmi_attnblk.hip).
+struct QkvFuse {
+  uint64_t* gran;   // [M][hkv][gran_stride] u64
+  int gran_stride;
+};
+
+template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW, int FUSE = 0>
+__device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_rt, int b, char* smem,
+                                          const QkvFuse& fz) {
   constexpr int K = W * NL * 64;
   constexpr int KC = K / 64;
   constexpr int NWV = G * W;
   constexpr int XROW = Img<K>::XROW;
   static_assert(RT == 8 || RT == 16, "row tile");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(!FUSE || EPI == ZMI_EPI_QKV, "only the QKV projection hands off in-launch");
 
   // block -> (column block, row tile): the row tiles of one column block take ids 8 apart
-  const int b = blockIdx.x;
   const int idx = b >> 3;
   const int cb = (idx / n_rt) * 8 + (b & 7), rt = idx - (idx / n_rt) * n_rt;
   if (cb >= n_cb) return;  // padding block: exits before any barrier
@@ -165,53 +176,46 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
   __builtin_amdgcn_sched_barrier(0);
   ZMI_GSTAMP(2);
 
-  // (3) LayerNorm, one wave per row: lane owns the 8-element chunks lane + 64 i of the row; fp32
-  // sums in a fixed lane order, DPP wave reduction, bf16-rounded result written back in place.
+  // (3) LayerNorm (zmi_common.h arithmetic): task (row, part) per wave, so the few rows of a decode
+  // step use every wave; partial sums meet in the segment-sum area (free until the MFMA chain).
   // Each pass re-reads its chunks from LDS (no row copy in VGPRs: the weight slice in flight
   // already holds 4 NL of them, and occupancy decides whether every workgroup of a wide GEMV is
   // resident at once).
   if (PRO == PRO_LN) {
-    constexpr int CPL = K / 512;
-    for (int r = wave; r < rows; r += NWV) {
-      bf16_t* xr = xs + r * XROW;
-      auto chunk_sum = [&](int i, float mean, bool sq) {
+    constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
+    float* part = red;  // [RT][NQ] sums, then [RT][NQ] squared deviations at + RT NQ
+    const int ntask = rows * NQ;
+    auto pass = [&](int task, float mean, bool sq) {
+      const int r = task / NQ, q = task - r * NQ;
+      const bf16_t* xr = xs + r * XROW + q * (K / NQ);
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i) t += ln_chunk_sum(*reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8), mean, sq);
+      return wave_sum(t);
+    };
+    for (int task = wave; task < ntask; task += NWV) {
+      const float v = pass(task, 0.f, false);
+      if (lane == 0) part[task] = v;
+    }
+    __syncthreads();
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ;
+      const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
+      const float v = pass(task, mean, true);
+      if (lane == 0) part[RT * NQ + task] = v;
+    }
+    __syncthreads();
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ, q = task - r * NQ;
+      const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
+      const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part + RT * NQ + r * NQ) / (float)K + a.eps), nbias = -mean * rstd;
+      bf16_t* xr = xs + r * XROW + q * (K / NQ);
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i) {
+        const int c = q * (K / NQ) / 8 + lane + 64 * i;
         const uint4 xv = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
-        const uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (sq) {
-            const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
-            t += d0 * d0 + d1 * d1;
-          } else {
-            t += bf2f(u[j]) + bf2f(u[j] >> 16);
-          }
-        }
-        return t;
-      };
-      float s = 0.f;
-#pragma unroll 2
-      for (int i = 0; i < CPL; ++i) s += chunk_sum(i, 0.f, false);
-      const float mean = wave_sum(s) / (float)K;
-      float ss = 0.f;
-#pragma unroll 2
-      for (int i = 0; i < CPL; ++i) ss += chunk_sum(i, mean, true);
-      const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)K + a.eps), nbias = -mean * rstd;
-#pragma unroll 2
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        const uint4 xv = *reinterpret_cast<const uint4*>(xr + c * 8);
-        const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
-        const uint4 gb = *reinterpret_cast<const uint4*>(bet + c * 8);
-        uint32_t u[4] = {xv.x, xv.y, xv.z, xv.w};
-        const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float y0 = (bf2f(u[j]) * rstd + nbias) * bf2f(uw[j]) + bf2f(ub[j]);
-          const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
-          u[j] = f2bf(y0) | (f2bf(y1) << 16);
-        }
-        *reinterpret_cast<uint4*>(xr + c * 8) = uint4{u[0], u[1], u[2], u[3]};
+        *reinterpret_cast<uint4*>(xr + (lane + 64 * i) * 8) = ln_apply(
+            xv, *reinterpret_cast<const uint4*>(gam + c * 8), *reinterpret_cast<const uint4*>(bet + c * 8), rstd, nbias);
       }
     }
     __syncthreads();
@@ -301,26 +305,44 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
         x1 = r1;
       }
       const uint32_t packed = f2bf(x0) | (f2bf(x1) << 16);
+      int gkh = 0, gslot = 0;  // granule of this pair (FUSE)
       if (n < qcols) {
         *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)(row0 + r) * a.ldo + n) = packed;
+        const int gq = a.hq / a.hkv;
+        gkh = n / (gq * a.hd);
+        gslot = (n - gkh * gq * a.hd) >> 1;
       } else if (n < qcols + kcols) {  // K cache [row][kv head][position][hd]
         const int nn = n - qcols, kh = nn / a.hd, d = nn - kh * a.hd;
         const size_t o = (((size_t)q_kvr * a.hkv + kh) * a.smax + q_pos) * a.hd + d;
         *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.k_cache) + o) = packed;
+        gkh = kh;
+        gslot = (a.hq / a.hkv) * (a.hd >> 1) + (d >> 1);
       } else {  // V cache, transposed: [row][kv head][hd][position] (zmi_attn.hip's P.V operand)
         const int nn = n - qcols - kcols, kh = nn / a.hd, d = nn - kh * a.hd;
         bf16_t* vt = reinterpret_cast<bf16_t*>(a.v_cache) + (((size_t)q_kvr * a.hkv + kh) * a.hd + d) * a.smax + q_pos;
         vt[0] = (bf16_t)(packed & 0xffffu);
         vt[a.smax] = (bf16_t)(packed >> 16);
+        gkh = kh;
+        gslot = (a.hq / a.hkv + 1) * (a.hd >> 1) + (d >> 1);
       }
+      if (FUSE)
+        st_wt64(fz.gran + ((size_t)(row0 + r) * a.hkv + gkh) * fz.gran_stride + gslot,
+                (uint64_t)packed | ((uint64_t)(unsigned)(q_pos + 1) << 32));
     }
   }
   ZMI_GSTAMP(6);
 }
 
-// (W, NL, RT) from K: K = 64 W NL. The LayerNorm'd K = 2048 projections stream 16 chunks per lane
-// from 2 waves per group; without LayerNorm 4 x 8 (round-1 measurements of the same streaming
-// structure, tools/bench_graph.py). K = 8192 holds 8 rows per tile (8 x 16 KiB of LDS).
+template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
+__global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemv_body<G, W, NL, RT, PRO, EPI, NTW>(a, n_cb, n_rt, blockIdx.x, smem, QkvFuse{nullptr, 0});
+}
+
+// (W, NL, RT) from K: K = 64 W NL. The shape fixes a row's reduction order, so it depends on K
+// only (every M, every launch form: decode, prefill and zmi_attn_block's QKV role agree bit for
+// bit). K = 2048 streams 8 chunks per lane from 4 waves per group (with G = 2: 512 threads, the
+// fused QKV + attention launch's block size); K = 8192 holds 8 rows per tile (8 x 16 KiB of LDS).
 struct Shape {
   int W, NL, RT;
 };
@@ -328,7 +350,7 @@ inline bool shape_for(int K, bool ln, Shape* s) {
   switch (K) {
     case 512: *s = {2, 4, 16}; return true;
     case 1024: *s = {4, 4, 16}; return true;
-    case 2048: *s = ln ? Shape{2, 16, 16} : Shape{4, 8, 16}; return true;
+    case 2048: *s = {4, 8, 16}; return true;
     case 4096: *s = {4, 16, 16}; return true;
     case 8192: *s = {8, 16, 8}; return true;
   }
@@ -336,10 +358,11 @@ inline bool shape_for(int K, bool ln, Shape* s) {
 }
 
 // column groups per block: 2 for the many-group LayerNorm'd projections (qkv, fc1, heads: the
-// block's LayerNorm and activation staging are then shared by 16 columns); `groups` > 0 overrides
+// block's LayerNorm and activation staging are then shared by 16 columns); `groups` > 0 overrides.
+// Speed only: a group's arithmetic does not depend on G.
 inline int groups_for(const ZmiGemvArgs& a, const Shape& s) {
   if (a.groups > 0) return a.groups;
-  return (s.W == 2 && s.NL == 16 && a.N / 8 >= 384) ? 2 : 1;
+  return (a.ln_w != nullptr && a.K == 2048 && a.N / 8 >= 384) ? 2 : 1;
 }
 
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
@@ -379,9 +402,8 @@ hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
   if (g == G_ && sh.W == W_ && sh.NL == NL_ && sh.RT == RT_) return launch_g<G_, W_, NL_, RT_, EPI>(a, s);
   ZMI_SHAPE(1, 2, 4, 16)
   ZMI_SHAPE(1, 4, 4, 16)
-  ZMI_SHAPE(1, 2, 16, 16)
-  ZMI_SHAPE(2, 2, 16, 16)
   ZMI_SHAPE(1, 4, 8, 16)
+  ZMI_SHAPE(2, 4, 8, 16)
   ZMI_SHAPE(1, 4, 16, 16)
   ZMI_SHAPE(1, 8, 16, 8)
 #undef ZMI_SHAPE

@@ -72,57 +72,46 @@ extern "C" int zmi_graph_destroy(void* graph_exec) {
 }
 
 // ---- LayerNorm of whole rows (nn.LayerNorm, reference zonos/backbone/_torch.py:62,88,90) -------------
-// One wave per row with the GEMV prologue's arithmetic (zmi_gemv_impl.h step 3): lane owns the 8-element
-// chunks lane + 64 i, fp32 two-pass statistics reduced by DPP in a fixed order, bf16 output. Used for
-// norm_f by the backbone plugin (zonos_vibes_amd/backbone.py); the decode step fuses its LayerNorms.
+// One wave per row, the parts of zmi_common.h's LayerNorm arithmetic in order (the GEMV prologue spreads
+// the same parts over waves: identical bits), bf16 output. Used for norm_f by the backbone plugin
+// (zonos_vibes_amd/backbone.py); the decode step fuses its LayerNorms.
 namespace {
 template <int CPL>
 __global__ __launch_bounds__(256) void layernorm_rows_kernel(const bf16_t* x, int ldx, int m, const bf16_t* w,
                                                              const bf16_t* b, float eps, bf16_t* out, int ldo) {
-  constexpr int K = CPL * 512;
+  constexpr int K = CPL * 512, NQ = ln_parts(K), CPQ = CPL / NQ;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= m) return;
   const bf16_t* xr = x + (size_t)r * ldx;
-  uint4 xv[CPL];
-  float s = 0.f;
+  uint4 xv[NQ][CPQ];
+  float p[NQ];
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    xv[i] = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
-    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+  for (int q = 0; q < NQ; ++q) {
     float t = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) t += bf2f(u[j]) + bf2f(u[j] >> 16);
-    s += t;
+    for (int i = 0; i < CPQ; ++i) {
+      xv[q][i] = *reinterpret_cast<const uint4*>(xr + q * (K / NQ) + (lane + 64 * i) * 8);
+      t += ln_chunk_sum(xv[q][i], 0.f, false);
+    }
+    p[q] = wave_sum(t);
   }
-  const float mean = wave_sum(s) / (float)K;
-  float ss = 0.f;
+  const float mean = ln_combine<NQ>(p) / (float)K;
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+  for (int q = 0; q < NQ; ++q) {
     float t = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float d0 = bf2f(u[j]) - mean, d1 = bf2f(u[j] >> 16) - mean;
-      t += d0 * d0 + d1 * d1;
-    }
-    ss += t;
+    for (int i = 0; i < CPQ; ++i) t += ln_chunk_sum(xv[q][i], mean, true);
+    p[q] = wave_sum(t);
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(ss) / (float)K + eps), nbias = -mean * rstd;
+  const float rstd = 1.0f / sqrtf(ln_combine<NQ>(p) / (float)K + eps), nbias = -mean * rstd;
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
-    const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
-    const uint32_t u[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-    const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
-    uint32_t o[4];
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float y0 = (bf2f(u[j]) * rstd + nbias) * bf2f(uw[j]) + bf2f(ub[j]);
-      const float y1 = (bf2f(u[j] >> 16) * rstd + nbias) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
-      o[j] = f2bf(y0) | (f2bf(y1) << 16);
+    for (int i = 0; i < CPQ; ++i) {
+      const int c = q * (K / NQ) / 8 + lane + 64 * i;
+      const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
+      reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = ln_apply(xv[q][i], gw, gb, rstd, nbias);
     }
-    reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = uint4{o[0], o[1], o[2], o[3]};
-  }
 }
 }  // namespace
 

@@ -94,6 +94,10 @@ class HipEngine:
         self.sptr = self.stream.cuda_stream
         self.w = None
         self.attn_variant = 0  # zmi_attention_variant kernel choice (0 = library; all give identical bits)
+        # decode QKV + attention as ONE launch (zmi_attn_block) where it applies: <= 16 rows and
+        # positions below the whole-query kernel's reach; identical bits either way (speed only)
+        self.attn_block = True
+        self.attn_block_slices = 8
         self._plans: dict[int, list] = {}
         self._graphs: dict[int, int] = {}
         self._alloc()
@@ -119,6 +123,10 @@ class HipEngine:
             nf = self.lib.zmi_attention_partial_floats(nq, self.H, self.Hkv, self.hd, self.smax - 1)
             self.attn_o = z(nf, dt=torch.float32)        # attention chunk partials (zmi_attn_merge.h)
             self.attn_lm = z(nf // self.hd * 2, dt=torch.float32)
+            # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer; a row's
+            # areas are zeroed when it starts an utterance (prefill), and its error word
+            self.blk_gran = z(self.L, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
+            self.blk_err = z(4, dt=torch.int32)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -221,19 +229,28 @@ class HipEngine:
         self._graphs.clear()
         self._plans.clear()
 
+    def _use_attn_block(self, rows: int) -> bool:
+        return (self.attn_block and rows <= 16 and self.d == 2048 and self.H == 4 * self.Hkv
+                and self.smax - 1 < self.lib.zmi_attention_max_keys_whole())
+
     def _plan(self, rows: int) -> list:
         """Decode-step launches for the first `rows` rows (slots 0 .. rows/2 - 1). Every kernel's
-        per-row arithmetic is independent of `rows`, so a slot decodes identically in any plan."""
+        per-row arithmetic is independent of `rows` and of the launch form, so a slot decodes
+        identically in any plan."""
         if rows not in self._plans:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
+            fused = self._use_attn_block(rows)
             plan = []
             for i, lw in enumerate(w["layers"]):
                 kv = (self.kc[i], self.vc[i])
-                plan.append(("gemv", self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                                ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv,
-                                                row_pos=self.row_pos)))
-                plan.append(("attn", i))
+                qkv = self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                 ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
+                if fused:
+                    plan.append(("attnblk", (qkv[0], i)))
+                else:
+                    plan.append(("gemv", qkv))
+                    plan.append(("attn", i))
                 plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
                 plan.append(("gemv", self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
                                                 self.F, ln=(lw["ln2_w"], lw["ln2_b"]))))
@@ -250,10 +267,18 @@ class HipEngine:
             self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(), self.attn_variant, self.sptr),
             "attention")
 
+    def _run_attn_block(self, item):
+        a, i = item
+        _lib.check(self.lib.zmi_attn_block(ctypes.byref(a), self.blk_gran[i].data_ptr(), self.blk_err.data_ptr(),
+                                           self.attn.data_ptr(), self.H * self.hd, self.attn_block_slices, self.sptr),
+                   "attn_block")
+
     def check_errors(self):
-        """Raise if an attention launch gave up waiting on a cross-block hand-off (bounded spin)."""
+        """Raise if an attention launch gave up waiting on an in-launch hand-off (bounded spin)."""
         if int(self.attn_work[:4].view(torch.int32).item()):
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
+        if int(self.blk_err[0].item()):
+            raise RuntimeError("attn_block: a wait for the QKV projection timed out (results are invalid)")
 
     def refresh_inputs(self):
         """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
@@ -283,6 +308,8 @@ class HipEngine:
         for kind, item in self._plan(rows):
             if kind == "gemv":
                 self._run_gemv(item)
+            elif kind == "attnblk":
+                self._run_attn_block(item)
             else:
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
                 self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
@@ -335,6 +362,7 @@ class HipEngine:
             sz = ctypes.sizeof(_lib.Sampling)
             self.params[slot * sz:(slot + 1) * sz].copy_(cp)
             _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
+            self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()  # no granule of an earlier utterance may match a tag
             xp = self.x_pre[: 2 * s_len]
             xp[:lc] = cond[0]
             xp[s_len: s_len + lc] = cond[1]
