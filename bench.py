@@ -64,7 +64,7 @@ def time_dominant_kernel(model, reps: int = 3):
     return us, bytes_launch
 
 
-FC1_KERNEL = "gemv_kernel<2, 2, 16, 16, 1, 3, 1>"  # G, W, NL, RT, PRO_LN, EPI_SWIGLU, non-temporal
+FC1_KERNEL = "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"  # G, W, NL, RT, PRO_LN, EPI_SWIGLU, non-temporal
 
 
 def pmc_traffic():
@@ -72,7 +72,7 @@ def pmc_traffic():
     rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950 correction; a counter pass
     serialises dispatches, so it is not repeated inside the timed run). None when the profile is
     absent or measured another kernel."""
-    path = os.path.join(REPO, "profiles", "r02_pmc_fc1_fetch.json")
+    path = os.path.join(REPO, "profiles", "r02b_pmc_fc1_fetch.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -357,10 +357,10 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv_kernel<G=2,W=2,NL=16,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": "gemv_kernel<G=2,W=4,NL=8,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
-                         "traffic_source": "profiles/r02_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "traffic_source": "profiles/r02b_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "utterance_breakdown": breakdown,
             "widened": widened,

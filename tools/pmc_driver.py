@@ -5,6 +5,7 @@ C2 mean position, on the synthetic Zonos-v0.1 engine (B = 1, two CFG rows).
     rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fc1 -o pmc -- \
         python tools/pmc_driver.py fc1
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attn        (and WRITE_SIZE)
+    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention)
 then tools/pmc_summary.py turns the counter CSV into the per-launch JSON kept under profiles/.
 """
 import os
@@ -40,6 +41,11 @@ def main(which: str, reps: int = 2):
         elif which == "attn":
             for i in range(e.L):
                 e._attention(i, e.q, 2, None, e.row_pos, e.smax - 1, e.attn)
+        elif which == "attnblk":  # the fused QKV + attention launch of every layer (granules fresh per rep)
+            e.blk_gran.zero_()
+            for kind, it in plan:
+                if kind == "attnblk":
+                    e._run_attn_block(it)
         else:
             raise SystemExit(f"unknown driver {which}")
     e.stream.synchronize()

@@ -20,9 +20,9 @@ pmc() {  # counter, driver, kernel substring, algorithmic bytes, tag
   f=$(find gpurun_out/pmc_$5 -name "*counter_collection.csv" -print -quit)
   python tools/pmc_summary.py "$f" "$3" $4 > $K/pmc_$5.json && rm -rf gpurun_out/pmc_$5
 }
-pmc FETCH_SIZE fc1 "gemv_kernel<2, 2, 16, 16, 1, 3, 1>" 67158016 fc1_fetch || exit $?
-pmc FETCH_SIZE attn attn_kernel 2424832 attn_fetch || exit $?
-pmc WRITE_SIZE attn attn_kernel 2424832 attn_write || exit $?
+pmc FETCH_SIZE fc1 "gemv_kernel<2, 4, 8, 16, 1, 3, 1>" 67158016 fc1_fetch || exit $?
+pmc FETCH_SIZE attnblk attn_block_kernel 15007744 attnblk_fetch || exit $?
+pmc WRITE_SIZE attnblk attn_block_kernel 15007744 attnblk_write || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
   --output-format csv -d gpurun_out/pmc_dac -o pmc -- python tools/bench_dac.py 861 > $K/pmc_dac.log 2>&1 || exit $?
 python tools/pmc_summary.py --mfma "$(find gpurun_out/pmc_dac -name "*counter_collection.csv" -print -quit)" \
