@@ -56,9 +56,17 @@ def main():
         rows.append(buf.view(4096, 8).cpu())
     e.check_errors()
     n_qkv = 192
+    # slot 7 of an attention block: shader-clock cycles (s_memtime) between stamps 3 and 4
+    cyc = torch.cat([st[n_qkv:][st[n_qkv:, 0] > 0][:, 7] for st in rows]).double()
+    dt = torch.cat([(st[n_qkv:][st[n_qkv:, 0] > 0][:, 4] - st[n_qkv:][st[n_qkv:, 0] > 0][:, 3]) for st in rows]).double()
+    print(json.dumps(dict(phase_3_to_4_cycles=float(cyc.median()), phase_3_to_4_us=float(dt.median()) / 100.0,
+                          shader_clock_GHz=round(float((cyc / (dt * 10.0)).median()), 3))), flush=True)
     out = {}
     for role, sl in (("qkv", slice(0, n_qkv)), ("attention", slice(n_qkv, 4096))):
         meds, maxs = [[] for _ in range(8)], [[] for _ in range(8)]
+        if role == "attention":
+            for st in rows:
+                st[:, 7] = 0
         for st in rows:
             live = st[:, 0] > 0
             t0 = st[live, 0].min()

@@ -287,62 +287,64 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   __syncthreads();
   ZMI_ASTAMP(2);
 
-  // (5) softmax statistics: tasks (chunk, head), wave + DNW i of them per wave, interleaved
+  // (5) softmax statistics: (chunk, head) tasks, wave + DNW i of them per wave. The chunk maxima
+  // are per-thread partials over 16-key segments (8 per chunk) folded by three DPP steps: max is
+  // exact in any order. e / l keep the chunked kernel's lane order and wave_sum.
   constexpr int NTASK = (XCH * XG + DNW - 1) / DNW;
   const int ntask = nc * XG;
-  {  // chunk maxima
-    float m[NTASK];
+  if (t < nc * XG * 8) {  // thread = (chunk, head, segment): t = ((c * XG + g) << 3) | seg
+    const int seg = t & 7, cg = t >> 3, c = cg / XG, g = cg - c * XG;
+    const int k0 = c * CH + 16 * seg;
+    const float4* p4 = reinterpret_cast<const float4*>(&sc[g][k0]);
+    float m = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < NTASK; ++i) {
-      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
-      m[i] = -INFINITY;
-      if (task < ntask) {
-#pragma unroll
-        for (int ii = 0; ii < CH / 64; ++ii) {
-          const int key = c * CH + lane + 64 * ii;
-          m[i] = fmaxf(m[i], key < nk ? sc[g][key] : -INFINITY);
-        }
-      }
+    for (int v = 0; v < 4; ++v) {
+      const float4 f = p4[v];
+      const int kb = k0 + 4 * v;
+      m = fmaxf(m, kb < nk ? f.x : -INFINITY);
+      m = fmaxf(m, kb + 1 < nk ? f.y : -INFINITY);
+      m = fmaxf(m, kb + 2 < nk ? f.z : -INFINITY);
+      m = fmaxf(m, kb + 3 < nk ? f.w : -INFINITY);
     }
-#pragma unroll
-    for (int i = 0; i < NTASK; ++i) m[i] = wave_max(m[i]);
-#pragma unroll
-    for (int i = 0; i < NTASK; ++i) {
-      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
-      if (task < ntask && lane == 0) mjc[c][g] = m[i];
-    }
+    m = fmaxf(m, dpp_mov<DPP_XOR1>(m));
+    m = fmaxf(m, dpp_mov<DPP_XOR2>(m));
+    m = fmaxf(m, dpp_mov<DPP_HALF_MIRROR>(m));  // lanes 8j .. 8j+7 now all hold the chunk maximum
+    if (seg == 0) mjc[c][g] = m;
   }
   __syncthreads();
   ZMI_ASTAMP(3);
+#ifdef ZMI_ATTN_STAMPS
+  const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
+#endif
   {  // M_j = max over the chunks of blocks 0..j; e = exp(s - M_j), l per chunk, P = bf16(e)
-    float l[NTASK];
 #pragma unroll
     for (int i = 0; i < NTASK; ++i) {
       const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
-      l[i] = 0.f;
-      if (task < ntask) {
+      if (task < ntask) {  // wave-uniform
         const int j = c / CPB, dep = min((j + 1) * CPB, nc);
-        const float M = wave_max(lane < dep ? mjc[lane][g] : -INFINITY);  // exact: max is order-free
+        float M = mjc[0][g];
+#pragma unroll
+        for (int cc = 1; cc < XCH; ++cc)  // unrolled: the LDS reads issue together
+          if (cc < dep) M = fmaxf(M, mjc[cc][g]);
         if (c % CPB == 0 && lane == 0) mblk[j][g] = M;
+        float l = 0.f;
 #pragma unroll
         for (int ii = 0; ii < CH / 64; ++ii) {
           const int key = c * CH + lane + 64 * ii;
           const float e = key < nk ? expf(sc[g][key] - M) : 0.f;
-          l[i] += e;
+          l += e;
           pb[g][key] = (bf16_t)f2bf(e);
         }
+        l = wave_sum(l);
+        if (lane == 0) ljc[c][g] = l;
       }
-    }
-#pragma unroll
-    for (int i = 0; i < NTASK; ++i) l[i] = wave_sum(l[i]);
-#pragma unroll
-    for (int i = 0; i < NTASK; ++i) {
-      const int task = wave + DNW * i, c = task / XG, g = task - c * XG;
-      if (task < ntask && lane == 0) ljc[c][g] = l[i];
     }
   }
   __syncthreads();
   ZMI_ASTAMP(4);
+#ifdef ZMI_ATTN_STAMPS
+  if (threadIdx.x == 0 && a.stamps) a.stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memtime() - cyc0;
+#endif
   // (6) workers: P.V of the slice's dims, each chunk's groups summed in group order in registers
   if (wave > 0) {
 #pragma unroll
@@ -397,15 +399,24 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   if (t < XG * DSD) {
     const int g = t / DSD, dl = t - g * DSD;
     float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
-    for (int c = 0; c < nc; ++c) {
-      const float oc = ocs[c][g][dl];
+    float ocv[XCH], lcv[XCH];
+#pragma unroll
+    for (int c = 0; c < XCH; ++c) {  // every read first (clamped rows past nc are never used)
+      const int cr = min(c, nc - 1);
+      ocv[c] = ocs[cr][g][dl];
+      lcv[c] = ljc[cr][g];
+    }
+#pragma unroll
+    for (int c = 0; c < XCH; ++c) {
+      if (c >= nc) break;
+      const float oc = ocv[c];
       if (c % CPB == 0) {
         ob = oc;
-        lb = ljc[c][g];
+        lb = lcv[c];
         mb = mblk[c / CPB][g];
       } else {
         ob += oc;
-        lb += ljc[c][g];
+        lb += lcv[c];
       }
       if (c % CPB == CPB - 1 || c == nc - 1) {
         if (c < CPB) {
