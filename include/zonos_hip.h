@@ -213,6 +213,41 @@ int zmi_prefix_condition(const ZmiCondParam* params, const ZmiCondRow* rows, int
                          const void* ln_w, const void* ln_b, float eps, void* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Hybrid backbone (Zonos-v0.1-hybrid, zonos/backbone/_mamba_ssm.py:9-57): the blocks mamba-ssm
+ * 2.2.4's create_block builds (Mamba2 mixer, MHA at attn_layer_idx, fused add + LayerNorm).
+ * mamba-ssm is not in this image: parity unpinned (oracle/hybrid_cpu.py restates it).
+ * ------------------------------------------------------------------------------------- */
+typedef struct ZmiMamba2Args {
+  const void* zxbcdt;   /* bf16 [M][ld_zx] in_proj output: z [d_ssm] | xBC [d_ssm + 2 d_state] | dt [nheads] */
+  int ld_zx, M;
+  int d_ssm, nheads, headdim, d_state, d_conv, ngroups; /* headdim 64, d_state 128, d_conv 4, ngroups 1 */
+  const void* conv_w;   /* bf16 [d_ssm + 2 d_state][d_conv] depthwise conv1d weight                  */
+  const void* conv_b;   /* bf16 [d_ssm + 2 d_state]                                                  */
+  const float* dt_bias; /* f32 [nheads]                                                              */
+  const float* A;       /* f32 [nheads] = -exp(A_log)                                                */
+  const float* D;       /* f32 [nheads]                                                              */
+  void* conv_ring;      /* bf16 [rows][d_conv][d_ssm + 2 d_state]: raw xBC of position q in slot q % 4 */
+  void* ssm;            /* bf16 [rows][nheads][headdim][d_state]                                    */
+  void* y;              /* bf16 [M][ldy] out: C.h + D x (before the gated norm)                      */
+  int ldy, reserved;
+  const int* row_pos;   /* [M] position of the row's token (< 0: inactive row; step only)           */
+  const int* row_kv;    /* [M] state row of each activation row (NULL: row m)                       */
+} ZmiMamba2Args;
+/* Decode: causal_conv1d_update + SiLU + selective_state_update(dt_softplus) for one token per row
+ * (mamba_ssm/modules/mamba2.py Mamba2.step). */
+int zmi_mamba2_step(const ZmiMamba2Args* args, void* stream);
+/* Prefill from an empty state: M / seq_len sequences of seq_len rows (causal_conv1d_fn +
+ * mamba_chunk_scan_combined of Mamba2.forward), leaving each sequence's final state and conv ring. */
+int zmi_mamba2_scan(const ZmiMamba2Args* args, int seq_len, void* stream);
+/* layer_norm_fn(hidden, w, b, residual, prenorm=True): s = hidden + residual (fp32; hidden may be NULL:
+ * s = residual), residual <- bf16(s) if store_residual, out = LayerNorm(s) bf16; k in {512 .. 4096}. */
+int zmi_add_layernorm(const void* hidden, int ldh, void* residual, int ldr, int m, int k, const void* w,
+                      const void* b, float eps, void* out, int ldo, int store_residual, void* stream);
+/* RMSNormGated(norm_before_gate=False): out = rmsnorm(y * silu(z)) * w, bf16; k in {512 .. 4096}. */
+int zmi_gated_rmsnorm(const void* y, int ldy, const void* z, int ldz, int m, int k, const void* w, float eps,
+                      void* out, int ldo, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Synthetic weights: fill with the counter-based uniform stream of zonos_vibes_amd/synthetic.py
  * dtype 0 = bf16, 1 = f32.
  * ------------------------------------------------------------------------------------- */

@@ -59,6 +59,17 @@ class CondRow(ctypes.Structure):
     _fields_ = [("param", c_int), ("kind", c_int), ("index", c_int), ("x_off", c_int)]
 
 
+class Mamba2Args(ctypes.Structure):
+    _fields_ = [
+        ("zxbcdt", c_void_p), ("ld_zx", c_int), ("M", c_int),
+        ("d_ssm", c_int), ("nheads", c_int), ("headdim", c_int), ("d_state", c_int), ("d_conv", c_int),
+        ("ngroups", c_int),
+        ("conv_w", c_void_p), ("conv_b", c_void_p), ("dt_bias", c_void_p), ("A", c_void_p), ("D", c_void_p),
+        ("conv_ring", c_void_p), ("ssm", c_void_p), ("y", c_void_p), ("ldy", c_int), ("reserved", c_int),
+        ("row_pos", c_void_p), ("row_kv", c_void_p),
+    ]
+
+
 COND_EMBED, COND_VECTOR, COND_FOURIER, COND_LINEAR, COND_PASSTHROUGH = range(5)
 
 
@@ -96,6 +107,12 @@ _SIGS = {
     "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p]),
     "zmi_prefix_condition": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                      c_void_p, c_void_p]),
+    "zmi_mamba2_step": (c_int, [ctypes.POINTER(Mamba2Args), c_void_p]),
+    "zmi_mamba2_scan": (c_int, [ctypes.POINTER(Mamba2Args), c_int, c_void_p]),
+    "zmi_add_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
+                                  c_void_p, c_int, c_int, c_void_p]),
+    "zmi_gated_rmsnorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_int,
+                                  c_void_p]),
     "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),
     "zmi_graph_begin": (c_int, [c_void_p]),
     "zmi_graph_end": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),

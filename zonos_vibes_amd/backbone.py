@@ -21,15 +21,13 @@ import torch
 
 from . import _lib
 from .config import BackboneConfig, InferenceParams, PrefixConditionerConfig, ZonosConfig
-from .engine import HipEngine
+from .engine import HipEngine, make_engine
 
 
 class HipZonosBackbone:
-    supported_architectures = ["transformer"]
+    supported_architectures = ["transformer", "hybrid"]
 
     def __init__(self, config: BackboneConfig, device="cuda"):
-        if config.ssm_cfg:
-            raise NotImplementedError("the hybrid (mamba-ssm) backbone is not built")
         self.config = config
         self.device = torch.device(device)
         self._cfg = ZonosConfig(config, PrefixConditionerConfig([], "none"))
@@ -43,15 +41,18 @@ class HipZonosBackbone:
             self.engine.load_state_dict(self._sd)
 
     def allocate_inference_cache(self, batch_size: int, max_seqlen: int, dtype=torch.bfloat16) -> dict:
-        """{layer: (K [B][Hkv][Smax][hd], V^T [B][Hkv][hd][Smax])} bf16 (_torch.py:64-71)."""
+        """{layer: (K [B][Hkv][Smax][hd], V^T [B][Hkv][hd][Smax])} bf16 (_torch.py:64-71); for the hybrid
+        (_mamba_ssm.py:38-42) Mamba2 layers hold (conv ring, SSM state) instead."""
         if dtype != torch.bfloat16:
             raise ValueError("the HIP backbone keeps its KV cache in bf16 (as the reference's generate does)")
         slots = (batch_size + 1) // 2
-        self.engine = HipEngine(self._cfg, self.device, max_slots=slots, max_seqlen=max_seqlen,
-                                max_prefill=slots * max_seqlen)
+        self.engine = make_engine(self._cfg, self.device, max_slots=slots, max_seqlen=max_seqlen,
+                                  max_prefill=slots * max_seqlen)
         if self._sd is not None:
             self.engine.load_state_dict(self._sd)
         e = self.engine
+        if e.hybrid:
+            return e.inference_cache()
         return {i: (e.kc[i], e.vc[i]) for i in range(e.L)}
 
     def forward(self, hidden_states: torch.Tensor, inference_params: InferenceParams) -> torch.Tensor:
@@ -68,6 +69,9 @@ class HipZonosBackbone:
         max_pos = inference_params.seqlen_offset + s - 1
         if max_pos >= e.smax:
             raise ValueError("positions beyond the allocated max_seqlen")
+        if e.hybrid and inference_params.seqlen_offset:
+            raise NotImplementedError("hybrid backbone plugin: prefill from position 0 only (decode runs inside "
+                                      "generate(), whose step fuses the heads and sampler)")
         e.stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(e.stream):
             e.x_pre[:m] = hidden_states.reshape(m, d).to(torch.bfloat16)
@@ -77,8 +81,7 @@ class HipZonosBackbone:
             e.row_kv_pre[:m] = torch.arange(b, dtype=torch.int32, device=self.device).repeat_interleave(s)
             e._prefill_layers(m, max_pos)
             out = torch.empty(m, d, dtype=torch.bfloat16, device=self.device)
-            _lib.check(e.lib.zmi_layernorm_rows(e.x_pre.data_ptr(), d, m, d, e.w["nf_w"].data_ptr(),
-                                                e.w["nf_b"].data_ptr(), e.eps, out.data_ptr(), d, e.sptr), "norm_f")
+            e.final_norm_pre(m, out)
         torch.cuda.current_stream(self.device).wait_stream(e.stream)
         e.check_errors()
         return out.view(b, s, d)

@@ -72,6 +72,27 @@ class BackboneConfig:
     def head_dim(self) -> int:
         return self.d_model // self.num_heads
 
+    @property
+    def is_hybrid(self) -> bool:
+        return bool(self.ssm_cfg)
+
+    def mamba2_dims(self) -> dict:
+        """Mamba2 mixer geometry from ssm_cfg with mamba-ssm 2.2.4's Mamba2 defaults (d_state 128,
+        d_conv 4, expand 2, headdim 64, ngroups 1): d_ssm = expand d_model, nheads = d_ssm / headdim,
+        in_proj width 2 d_ssm + 2 ngroups d_state + nheads (mamba_ssm/modules/mamba2.py)."""
+        c = dict(self.ssm_cfg)
+        if c.get("layer", "Mamba1") != "Mamba2":
+            raise NotImplementedError("only Mamba2 mixers are built (Zonos-v0.1-hybrid uses ssm_cfg layer=Mamba2)")
+        d_ssm = int(c.get("d_ssm") or c.get("expand", 2) * self.d_model)
+        hd = int(c.get("headdim", 64))
+        out = dict(d_ssm=d_ssm, headdim=hd, nheads=d_ssm // hd, d_state=int(c.get("d_state", 128)),
+                   d_conv=int(c.get("d_conv", 4)), ngroups=int(c.get("ngroups", 1)),
+                   rmsnorm=bool(c.get("rmsnorm", True)), norm_before_gate=bool(c.get("norm_before_gate", False)),
+                   D_has_hdim=bool(c.get("D_has_hdim", False)))
+        out["conv_dim"] = d_ssm + 2 * out["ngroups"] * out["d_state"]
+        out["d_in_proj"] = 2 * d_ssm + 2 * out["ngroups"] * out["d_state"] + out["nheads"]
+        return out
+
 
 @dataclass
 class PrefixConditionerConfig:
@@ -119,7 +140,35 @@ def tiny_transformer(n_layer: int = 2) -> ZonosConfig:
     return transformer_config(512, n_layer, 4, 1, 1024)
 
 
+def hybrid_config(d_model: int, n_layer: int, attn_layer_idx: list, num_heads: int, num_heads_kv: int,
+                  d_intermediate: int = 0, attn_mlp_d_intermediate: int = 0, eps: float = 1e-5) -> ZonosConfig:
+    """A hybrid-backbone `ZonosConfig` (reference MambaSSMZonosBackbone, _mamba_ssm.py:9-57): Mamba2 mixers,
+    MHA mixers at attn_layer_idx (mamba_ssm MHA: non-interleaved rotary over the whole head)."""
+    bb = BackboneConfig(
+        d_model=d_model, d_intermediate=d_intermediate, attn_mlp_d_intermediate=attn_mlp_d_intermediate,
+        n_layer=n_layer, ssm_cfg={"layer": "Mamba2"}, attn_layer_idx=list(attn_layer_idx),
+        attn_cfg={"causal": True, "num_heads": num_heads, "num_heads_kv": num_heads_kv,
+                  "rotary_emb_dim": d_model // num_heads, "qkv_proj_bias": False, "out_proj_bias": False},
+        rms_norm=False, residual_in_fp32=False, norm_epsilon=eps)
+    return ZonosConfig(bb, PrefixConditionerConfig([], "none"))
+
+
+def zonos_v01_hybrid() -> ZonosConfig:
+    """Zonos-v0.1-hybrid dims as published in its config.json (d 2048, 46 layers, Mamba2 mixers, MHA 16/4
+    heads at layers 9/18/27/36/45, no MLPs). Not verifiable offline (no checkpoint or config in the
+    reference tree): the kernels take the dims from whatever config.json is loaded."""
+    return hybrid_config(2048, 46, [9, 18, 27, 36, 45], 16, 4)
+
+
+def tiny_hybrid(n_layer: int = 4, attn_layer_idx=(2,), d_intermediate: int = 0,
+                attn_mlp_d_intermediate: int = 0) -> ZonosConfig:
+    """Small hybrid for parity tests: d 512 (d_ssm 1024, 16 Mamba2 heads), MHA 4/1 heads x 128."""
+    return hybrid_config(512, n_layer, list(attn_layer_idx), 4, 1, d_intermediate, attn_mlp_d_intermediate)
+
+
 PRESETS = {
     "zonos-v0.1-transformer": zonos_v01_transformer,
+    "zonos-v0.1-hybrid": zonos_v01_hybrid,
     "tiny": tiny_transformer,
+    "tiny-hybrid": tiny_hybrid,
 }

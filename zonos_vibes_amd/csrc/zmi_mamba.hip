@@ -1,0 +1,370 @@
+// Hybrid backbone kernels (Zonos-v0.1-hybrid, BASELINE config C4), gfx950.
+//
+// Reference: zonos/backbone/_mamba_ssm.py:9-57 builds its layers with mamba-ssm 2.2.4's
+// `create_block` (absent from this image, so parity is unpinned; oracle/hybrid_cpu.py restates the
+// published algorithm). A decode step of one Mamba2 block is
+//
+//   hidden, residual = layer_norm_fn(hidden, norm.w, norm.b, residual, prenorm=True)  (Block.forward)
+//   zxbcdt = in_proj(hidden)                                                            (GEMV kernel)
+//   xBC    = silu(causal_conv1d_update(xBC, conv_state, conv1d.w, conv1d.b))            (mamba2_step)
+//   y      = selective_state_update(ssm_state, x, dt, A, B, C, D, dt_bias, softplus)    (mamba2_step)
+//   y      = RMSNormGated(y, z)                                                         (gated_rmsnorm)
+//   out    = out_proj(y)                                                                (GEMV kernel)
+//
+// and the prefill is the same block over a whole sequence (causal_conv1d_fn + mamba_chunk_scan_combined;
+// mamba2_scan here: the recurrence in fp32 registers, one workgroup per (sequence, head)).
+//
+// State layouts (this library's, not the reference's roll buffer):
+//   conv ring  bf16 [row][4][conv_dim]: the raw xBC input of position q sits in slot q & 3. A step at
+//              position p reads slots of p-3 .. p-1 and writes slot p & 3 (that of p-4, which nobody
+//              reads), so the workgroups of one row never race; negative positions read as zero.
+//   ssm state  bf16 [row][nheads][headdim 64][d_state 128] (the reference keeps it in the cache dtype).
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+
+namespace {
+
+constexpr int MB_HD = 64;    // headdim
+constexpr int MB_DS = 128;   // d_state (ngroups = 1)
+constexpr int MB_DC = 4;     // d_conv
+constexpr int MB_NT = 256;   // threads: (p = t / 4, n-quarter = t % 4)
+constexpr int MB_NCH = MB_HD + 2 * MB_DS;  // conv channels one head needs: its x, then B, C
+
+__device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
+// mamba_ssm/ops/triton/softplus.py; selective_state_update applies it below 20 only
+__device__ __forceinline__ float softplus_f(float v) { return v <= 20.f ? log1pf(expf(v)) : v; }
+
+// xBC channel index of local conv channel i of head h
+__device__ __forceinline__ int conv_channel(int i, int h, int d_ssm) {
+  return i < MB_HD ? h * MB_HD + i : d_ssm + (i - MB_HD);
+}
+
+// causal depthwise conv1d of one channel: bias first, taps oldest first, fp32 (causal_conv1d
+// update / fwd kernels), then SiLU; the caller rounds to bf16 (the conv output tensor is bf16)
+__device__ __forceinline__ float conv4(const bf16_t* w4, float bias, float x0, float x1, float x2, float x3) {
+  float acc = bias;
+  acc = fmaf(bf2f(w4[0]), x0, acc);
+  acc = fmaf(bf2f(w4[1]), x1, acc);
+  acc = fmaf(bf2f(w4[2]), x2, acc);
+  acc = fmaf(bf2f(w4[3]), x3, acc);
+  return silu_f(acc);
+}
+
+// ---------------------------------------------------------------------------- decode step
+__global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args a) {
+  const int m = blockIdx.x / a.nheads, h = blockIdx.x - m * a.nheads;
+  const int pos = a.row_pos[m];
+  if (pos < 0) return;
+  const int kv = a.row_kv ? a.row_kv[m] : m;
+  const int conv_dim = a.d_ssm + 2 * MB_DS;
+  const bf16_t* zx = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)m * a.ld_zx;
+  const bf16_t* xin = zx + a.d_ssm;  // z | xBC | dt
+  bf16_t* ring = reinterpret_cast<bf16_t*>(a.conv_ring) + (size_t)kv * MB_DC * conv_dim;
+  const bf16_t* cw = reinterpret_cast<const bf16_t*>(a.conv_w);
+  const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
+  __shared__ float xs[MB_HD], bc[2 * MB_DS];
+  const int t = threadIdx.x;
+
+  // (1) conv + SiLU of this head's 64 x channels and the 256 B / C channels (every head recomputes
+  // B / C; head 0 alone writes their ring slot)
+  for (int i = t; i < MB_NCH; i += MB_NT) {
+    const int c = conv_channel(i, h, a.d_ssm);
+    float v[MB_DC - 1];
+#pragma unroll
+    for (int k = 0; k < MB_DC - 1; ++k) {
+      const int q = pos - (MB_DC - 1) + k;
+      v[k] = q >= 0 ? bf2f(ring[(size_t)(q & 3) * conv_dim + c]) : 0.f;
+    }
+    const bf16_t raw = xin[c];
+    const float o = bfround(conv4(cw + (size_t)c * MB_DC, bf2f(cb[c]), v[0], v[1], v[2], bf2f(raw)));
+    if (i < MB_HD) xs[i] = o; else bc[i - MB_HD] = o;
+    if (i < MB_HD || h == 0) ring[(size_t)(pos & 3) * conv_dim + c] = raw;
+  }
+  // (2) dt = softplus(dt + dt_bias), dA = exp(A dt)  (selective_state_update, tie_hdim)
+  const float dtv = softplus_f(bf2f(zx[2 * a.d_ssm + 2 * MB_DS + h]) + a.dt_bias[h]);
+  const float dA = expf(a.A[h] * dtv);
+  __syncthreads();
+
+  // (3) state update and readout: lane (p, quarter) owns state[p][32 quarter .. +31]
+  const int p = t >> 2, nq = t & 3;
+  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
+  uint4 sv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sv[j] = reinterpret_cast<const uint4*>(st)[j];
+  const float x = xs[p];
+  const float* B = bc + nq * 32;
+  const float* C = bc + MB_DS + nq * 32;
+  float out = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t w[4] = {sv[j].x, sv[j].y, sv[j].z, sv[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = 8 * j + 2 * e;
+      float s0 = bf2f(w[e]), s1 = bf2f(w[e] >> 16);
+      s0 = s0 * dA + (B[n] * dtv) * x;
+      s1 = s1 * dA + (B[n + 1] * dtv) * x;
+      out += s0 * C[n];
+      out += s1 * C[n + 1];
+      w[e] = f2bf(s0) | (f2bf(s1) << 16);
+    }
+    sv[j] = uint4{w[0], w[1], w[2], w[3]};
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = sv[j];
+  out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
+  if (nq == 0)
+    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * a.D[h]);
+}
+
+// ---------------------------------------------------------------------------- prefill scan
+constexpr int SC_TT = 32;  // positions staged per tile
+
+__global__ __launch_bounds__(MB_NT) void mamba2_scan_kernel(const ZmiMamba2Args a, int seq_len) {
+  const int sq = blockIdx.x / a.nheads, h = blockIdx.x - sq * a.nheads;
+  const int row0 = sq * seq_len;
+  const int kv = a.row_kv ? a.row_kv[row0] : sq;
+  const int conv_dim = a.d_ssm + 2 * MB_DS;
+  const bf16_t* zx0 = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)row0 * a.ld_zx;
+  const bf16_t* cw = reinterpret_cast<const bf16_t*>(a.conv_w);
+  const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
+  __shared__ float xs[SC_TT][MB_HD], bs[SC_TT][MB_DS], cs[SC_TT][MB_DS], dts[SC_TT], das[SC_TT];
+  const int t = threadIdx.x, p = t >> 2, nq = t & 3;
+  const float Ah = a.A[h], Dh = a.D[h], dtb = a.dt_bias[h];
+  auto raw = [&](int q, int c) { return q >= 0 ? bf2f(zx0[(size_t)q * a.ld_zx + a.d_ssm + c]) : 0.f; };
+
+  float s[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) s[j] = 0.f;
+  for (int t0 = 0; t0 < seq_len; t0 += SC_TT) {
+    const int nt = min(SC_TT, seq_len - t0);
+    __syncthreads();  // the previous tile's readers are done
+    for (int idx = t; idx < nt * MB_NCH; idx += MB_NT) {
+      const int tt = idx / MB_NCH, i = idx - tt * MB_NCH, q = t0 + tt;
+      const int c = conv_channel(i, h, a.d_ssm);
+      const float o = bfround(conv4(cw + (size_t)c * MB_DC, bf2f(cb[c]), raw(q - 3, c), raw(q - 2, c), raw(q - 1, c),
+                                    raw(q, c)));
+      if (i < MB_HD) xs[tt][i] = o;
+      else if (i < MB_HD + MB_DS) bs[tt][i - MB_HD] = o;
+      else cs[tt][i - MB_HD - MB_DS] = o;
+    }
+    if (t < nt) {
+      const float dtv = softplus_f(bf2f(zx0[(size_t)(t0 + t) * a.ld_zx + 2 * a.d_ssm + 2 * MB_DS + h]) + dtb);
+      dts[t] = dtv;
+      das[t] = expf(Ah * dtv);
+    }
+    __syncthreads();
+    for (int tt = 0; tt < nt; ++tt) {
+      const float x = xs[tt][p], dtv = dts[tt], dA = das[tt];
+      const float4* B4 = reinterpret_cast<const float4*>(&bs[tt][nq * 32]);
+      const float4* C4 = reinterpret_cast<const float4*>(&cs[tt][nq * 32]);
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 b = B4[j], c = C4[j];
+        s[4 * j + 0] = s[4 * j + 0] * dA + (b.x * dtv) * x;
+        s[4 * j + 1] = s[4 * j + 1] * dA + (b.y * dtv) * x;
+        s[4 * j + 2] = s[4 * j + 2] * dA + (b.z * dtv) * x;
+        s[4 * j + 3] = s[4 * j + 3] * dA + (b.w * dtv) * x;
+        out += s[4 * j + 0] * c.x;
+        out += s[4 * j + 1] * c.y;
+        out += s[4 * j + 2] * c.z;
+        out += s[4 * j + 3] * c.w;
+      }
+      out = quad_sum(out);
+      if (nq == 0)
+        reinterpret_cast<bf16_t*>(a.y)[(size_t)(row0 + t0 + tt) * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * Dh);
+    }
+  }
+  // final state (bf16, the cache dtype) and the ring slots of the last four positions (zero below 0)
+  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = f2bf(s[8 * j + 2 * e]) | (f2bf(s[8 * j + 2 * e + 1]) << 16);
+    reinterpret_cast<uint4*>(st)[j] = uint4{w[0], w[1], w[2], w[3]};
+  }
+  bf16_t* ring = reinterpret_cast<bf16_t*>(a.conv_ring) + (size_t)kv * MB_DC * conv_dim;
+  for (int idx = t; idx < MB_DC * MB_NCH; idx += MB_NT) {
+    const int k = idx / MB_NCH, i = idx - k * MB_NCH;
+    if (i >= MB_HD && h != 0) continue;
+    const int q = seq_len - MB_DC + k, c = conv_channel(i, h, a.d_ssm);
+    ring[(size_t)(q & 3) * conv_dim + c] = q >= 0 ? zx0[(size_t)q * a.ld_zx + a.d_ssm + c] : (bf16_t)0;
+  }
+}
+
+// ---------------------------------------------------------------------------- add + LayerNorm
+// layer_norm_fn(x, w, b, residual, prenorm=True, residual_in_fp32=False) (mamba_ssm/ops/triton/
+// layer_norm.py): s = x + residual in fp32; residual_out = bf16(s); y = (s - mean) * rstd * w + b on the
+// fp32 sum (two-pass statistics). One wave per row, lane L owns the 8-element chunks 8 (L + 64 i).
+template <int CPL>
+__global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh, bf16_t* res, int ldr, int m,
+                                                     const bf16_t* w, const bf16_t* b, float eps, bf16_t* out, int ldo,
+                                                     int store_res) {
+  constexpr int K = CPL * 512;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= m) return;
+  float v[CPL][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const uint4 rv = reinterpret_cast<const uint4*>(res + (size_t)r * ldr)[c];
+    uint32_t u[4] = {rv.x, rv.y, rv.z, rv.w};
+    uint32_t hu[4] = {0u, 0u, 0u, 0u};
+    if (hid) {
+      const uint4 hv = reinterpret_cast<const uint4*>(hid + (size_t)r * ldh)[c];
+      hu[0] = hv.x; hu[1] = hv.y; hu[2] = hv.z; hu[3] = hv.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[i][2 * e] = hid ? bf2f(hu[e]) + bf2f(u[e]) : bf2f(u[e]);
+      v[i][2 * e + 1] = hid ? bf2f(hu[e] >> 16) + bf2f(u[e] >> 16) : bf2f(u[e] >> 16);
+      sum += v[i][2 * e] + v[i][2 * e + 1];
+    }
+    if (store_res && hid) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = f2bf(v[i][2 * e]) | (f2bf(v[i][2 * e + 1]) << 16);
+      reinterpret_cast<uint4*>(res + (size_t)r * ldr)[c] = uint4{u[0], u[1], u[2], u[3]};
+    }
+  }
+  const float mean = wave_sum(sum) / (float)K;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean;
+      sq += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
+    const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float y0 = ((v[i][2 * e] - mean) * rstd) * bf2f(uw[e]) + bf2f(ub[e]);
+      const float y1 = ((v[i][2 * e + 1] - mean) * rstd) * bf2f(uw[e] >> 16) + bf2f(ub[e] >> 16);
+      o[e] = f2bf(y0) | (f2bf(y1) << 16);
+    }
+    reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+// ---------------------------------------------------------------------------- gated RMSNorm
+// RMSNormGated(norm_before_gate=False, one group) (mamba_ssm/ops/triton/layernorm_gated.py):
+// g = y * (z * sigmoid(z)) in fp32, out = g * rstd * w with rstd = 1 / sqrt(mean(g^2) + eps), bf16.
+// One wave per row, lane L owns the 8-element chunks 8 (L + 64 i).
+template <int CPL>
+__global__ __launch_bounds__(256) void gated_rms_kernel(const bf16_t* y, int ldy, const bf16_t* z, int ldz, int m,
+                                                        const bf16_t* w, float eps, bf16_t* out, int ldo) {
+  constexpr int K = CPL * 512;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= m) return;
+  float g[CPL][8];
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const uint4 yv = reinterpret_cast<const uint4*>(y + (size_t)r * ldy)[c];
+    const uint4 zv = reinterpret_cast<const uint4*>(z + (size_t)r * ldz)[c];
+    const uint32_t uy[4] = {yv.x, yv.y, yv.z, yv.w}, uz[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float zz = bf2f(uz[e >> 1] >> (16 * (e & 1)));
+      const float sg = 1.0f / (1.0f + expf(-zz));
+      g[i][e] = bf2f(uy[e >> 1] >> (16 * (e & 1))) * (zz * sg);
+      sq += g[i][e] * g[i][e];
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    const uint4 gw = reinterpret_cast<const uint4*>(w)[c];
+    const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      o[e] = f2bf((g[i][2 * e] * rstd) * bf2f(uw[e])) | (f2bf((g[i][2 * e + 1] * rstd) * bf2f(uw[e] >> 16)) << 16);
+    reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = uint4{o[0], o[1], o[2], o[3]};
+  }
+}
+
+int check_mamba(const ZmiMamba2Args* a) {
+  if (!a || !a->zxbcdt || !a->conv_w || !a->conv_b || !a->dt_bias || !a->A || !a->D || !a->conv_ring || !a->ssm ||
+      !a->y || !a->row_pos)
+    return zmi_fail_msg("mamba2: missing buffers");
+  if (a->headdim != MB_HD || a->d_state != MB_DS || a->d_conv != MB_DC || a->ngroups != 1)
+    return zmi_fail_msg("mamba2: built for headdim 64, d_state 128, d_conv 4, ngroups 1");
+  if (a->nheads <= 0 || a->d_ssm != a->nheads * MB_HD) return zmi_fail_msg("mamba2: d_ssm = nheads x 64");
+  if (a->ld_zx < 2 * a->d_ssm + 2 * MB_DS + a->nheads || a->ldy < a->d_ssm)
+    return zmi_fail_msg("mamba2: ld_zx >= 2 d_ssm + 2 d_state + nheads, ldy >= d_ssm");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int zmi_mamba2_step(const ZmiMamba2Args* a, void* stream) {
+  if (int e = check_mamba(a)) return e;
+  if (a->M <= 0) return 0;
+  hipLaunchKernelGGL(mamba2_step_kernel, dim3((unsigned)(a->M * a->nheads)), dim3(MB_NT), 0, (hipStream_t)stream, *a);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_mamba2_scan(const ZmiMamba2Args* a, int seq_len, void* stream) {
+  if (int e = check_mamba(a)) return e;
+  if (seq_len <= 0 || a->M % seq_len) return zmi_fail_msg("mamba2_scan: M must be a multiple of seq_len > 0");
+  hipLaunchKernelGGL(mamba2_scan_kernel, dim3((unsigned)(a->M / seq_len * a->nheads)), dim3(MB_NT), 0,
+                     (hipStream_t)stream, *a, seq_len);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_add_layernorm(const void* hidden, int ldh, void* residual, int ldr, int m, int k, const void* w,
+                                 const void* b, float eps, void* out, int ldo, int store_residual, void* stream) {
+  if (ldh % 8 || ldr % 8 || ldo % 8) return zmi_fail_msg("add_layernorm: leading dimensions must be multiples of 8");
+  if (!residual || !w || !b || !out) return zmi_fail_msg("add_layernorm: missing buffers");
+  if (m <= 0) return 0;
+  const dim3 grid((m + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+#define ZMI_ADDLN(CPL)                                                                                         \
+  hipLaunchKernelGGL(add_ln_kernel<CPL>, grid, dim3(256), 0, s, (const bf16_t*)hidden, ldh, (bf16_t*)residual, \
+                     ldr, m, (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo, store_residual)
+  switch (k) {
+    case 512: ZMI_ADDLN(1); break;
+    case 1024: ZMI_ADDLN(2); break;
+    case 2048: ZMI_ADDLN(4); break;
+    case 4096: ZMI_ADDLN(8); break;
+    default: return zmi_fail_msg("add_layernorm: k must be 512, 1024, 2048 or 4096");
+  }
+#undef ZMI_ADDLN
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_gated_rmsnorm(const void* y, int ldy, const void* z, int ldz, int m, int k, const void* w,
+                                 float eps, void* out, int ldo, void* stream) {
+  if (ldy % 8 || ldz % 8 || ldo % 8) return zmi_fail_msg("gated_rmsnorm: leading dimensions must be multiples of 8");
+  if (!y || !z || !w || !out) return zmi_fail_msg("gated_rmsnorm: missing buffers");
+  if (m <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+#define ZMI_GRMS(CPL)                                                                                          \
+  hipLaunchKernelGGL(gated_rms_kernel<CPL>, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, (const bf16_t*)y, ldy, \
+                     (const bf16_t*)z, ldz, m, (const bf16_t*)w, eps, (bf16_t*)out, ldo)
+  switch (k) {
+    case 512: ZMI_GRMS(1); break;
+    case 1024: ZMI_GRMS(2); break;
+    case 2048: ZMI_GRMS(4); break;
+    case 4096: ZMI_GRMS(8); break;
+    default: return zmi_fail_msg("gated_rmsnorm: k must be 512, 1024, 2048 or 4096");
+  }
+#undef ZMI_GRMS
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

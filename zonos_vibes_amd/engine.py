@@ -71,11 +71,13 @@ def _round8(n: int) -> int:
 
 
 class HipEngine:
+    hybrid = False
+
     def __init__(self, cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
                  max_prefill: int = 512):
         bb = cfg.backbone
-        if bb.ssm_cfg:
-            raise NotImplementedError("hybrid (mamba-ssm) backbone is not built (SURVEY.md §8f next #1)")
+        if bb.ssm_cfg and not self.hybrid:
+            raise ValueError("hybrid (mamba-ssm) configs run on HybridEngine (make_engine picks it)")
         self.cfg = cfg
         self.dev = torch.device(device)
         self.d, self.L, self.H, self.Hkv = bb.d_model, bb.n_layer, bb.num_heads, bb.num_heads_kv
@@ -100,7 +102,12 @@ class HipEngine:
         self.attn_block_slices = 8
         self._plans: dict[int, list] = {}
         self._graphs: dict[int, int] = {}
+        self.n_kv = self._kv_layers()
         self._alloc()
+
+    def _kv_layers(self) -> int:
+        """Layers with a KV cache (every layer of the transformer)."""
+        return self.L
 
     # ------------------------------------------------------------------ allocation
     def _alloc(self):
@@ -113,8 +120,8 @@ class HipEngine:
             self.logits = z(R, N_CODEBOOKS, 1026, dt=torch.float32)
             self.row_kv = z(R, dt=torch.int32)
             self.row_pos = torch.full((R,), -1, dtype=torch.int32, device=dev)  # every row inactive
-            self.kc = z(self.L, R, self.Hkv, self.smax, self.hd)   # K  [layer][row][kv head][position][hd]
-            self.vc = z(self.L, R, self.Hkv, self.hd, self.smax)   # V^T [layer][row][kv head][hd][position]
+            self.kc = z(self.n_kv, R, self.Hkv, self.smax, self.hd)   # K  [layer][row][kv head][position][hd]
+            self.vc = z(self.n_kv, R, self.Hkv, self.hd, self.smax)   # V^T [layer][row][kv head][hd][position]
             nq = max(R, 2 * self.max_prefill)
             wb = self.lib.zmi_attention_work_bytes(nq, self.H, self.Hkv, self.hd, self.smax - 1)
             if wb < 0:
@@ -125,7 +132,7 @@ class HipEngine:
             self.attn_lm = z(nf // self.hd * 2, dt=torch.float32)
             # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer; a row's
             # areas are zeroed when it starts an utterance (prefill), and its error word
-            self.blk_gran = z(self.L, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
+            self.blk_gran = z(self.n_kv, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
             self.blk_err = z(4, dt=torch.int32)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
@@ -310,9 +317,11 @@ class HipEngine:
                 self._run_gemv(item)
             elif kind == "attnblk":
                 self._run_attn_block(item)
-            else:
+            elif kind == "attn":
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
                 self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
+            else:  # "call": a prepared launch (hybrid kernels)
+                item()
         self._sample(self.logits, noise, 0, 0, rows // 2)
 
     def capture(self, slots: int | None = None):
@@ -375,16 +384,27 @@ class HipEngine:
             self.row_kv_pre[:s_len] = 2 * slot
             self.row_kv_pre[s_len: 2 * s_len] = 2 * slot + 1
             self._prefill_layers(2 * s_len, s_len - 1)
-            self.x_last[0] = xp[s_len - 1]
-            self.x_last[1] = xp[2 * s_len - 1]
-            self._run_gemv(self._gemv(self.w["heads"], self.x_last, 2, HEADS_N_PAD, d, _lib.EPI_LOGITS,
-                                      self.logits_pre, 0, n_valid=HEADS_N, ln=(self.w["nf_w"], self.w["nf_b"])))
+            self._prefill_logits(s_len)
             vals = {"active": 1, "pos": s_len, "offset": p, "remaining": max_new_tokens + 8, "stopping": 0,
                     "step": 0, "total_len": total}
             for k, v in vals.items():
                 st[k][slot] = v
             self._sample(self.logits_pre, noise, 1, slot, 1)
         return s_len
+
+    def _prefill_logits(self, s_len: int):
+        """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""
+        xp = self.x_pre
+        self.x_last[0] = xp[s_len - 1]
+        self.x_last[1] = xp[2 * s_len - 1]
+        self._run_gemv(self._gemv(self.w["heads"], self.x_last, 2, HEADS_N_PAD, self.d, _lib.EPI_LOGITS,
+                                  self.logits_pre, 0, n_valid=HEADS_N, ln=(self.w["nf_w"], self.w["nf_b"])))
+
+    def final_norm_pre(self, m: int, out: torch.Tensor):
+        """norm_f of the first m prefill rows into out (the backbone plugin's output)."""
+        _lib.check(self.lib.zmi_layernorm_rows(self.x_pre.data_ptr(), self.d, m, self.d, self.w["nf_w"].data_ptr(),
+                                               self.w["nf_b"].data_ptr(), self.eps, out.data_ptr(), self.d, self.sptr),
+                   "norm_f")
 
     def _prefill_layers(self, m: int, max_pos: int):
         """The m = 2 x S prefill rows through every layer, with the decode step's kernels (same per-row
@@ -425,3 +445,12 @@ class HipEngine:
         with torch.cuda.stream(self.stream):
             self.st["active"][slot] = 0
             self.row_pos[2 * slot: 2 * slot + 2] = -1
+
+
+def make_engine(cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
+                max_prefill: int = 512) -> HipEngine:
+    """The engine for a config's backbone: HipEngine (transformer) or HybridEngine (Mamba2 + MHA)."""
+    if cfg.backbone.ssm_cfg:
+        from .hybrid import HybridEngine
+        return HybridEngine(cfg, device, max_slots, max_seqlen, max_prefill)
+    return HipEngine(cfg, device, max_slots, max_seqlen, max_prefill)

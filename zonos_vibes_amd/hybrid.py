@@ -1,0 +1,264 @@
+"""HybridEngine: the Zonos-v0.1-hybrid backbone (Mamba2 + attention) on the HIP kernels.
+
+Reference: zonos/backbone/_mamba_ssm.py:9-57 (MambaSSMZonosBackbone), whose blocks come from
+mamba-ssm 2.2.4's create_block (absent here: parity unpinned, oracle/hybrid_cpu.py). Everything
+around the backbone — delay pattern, prefill orchestration, heads, CFG, sampler, EOS state machine,
+hipGraph-captured decode loop, slots — is HipEngine's; this class only swaps the layer plan:
+
+  every block    zmi_add_layernorm (layer_norm_fn prenorm: residual += hidden in fp32, LayerNorm)
+  Mamba2 block   in_proj GEMV -> zmi_mamba2_step (conv ring + SiLU + selective state update)
+                 -> zmi_gated_rmsnorm -> out_proj GEMV      (prefill: zmi_mamba2_scan over the sequence)
+  MHA block      QKV GEMV (non-interleaved rotary as interleaved pairs on permuted q / k rows, bf16
+                 cos / sin as flash-attn caches them) -> attention kernel -> out_proj GEMV
+  optional MLP   zmi_add_layernorm -> fc1 SwiGLU GEMV -> fc2 GEMV       (d_intermediate > 0)
+  norm_f         zmi_add_layernorm (hidden + residual) -> heads GEMV
+
+State per slot row: the conv ring bf16 [4][conv_dim] and the SSM state bf16 [nheads][64][128] of
+every Mamba2 layer (1.06 MB per row and layer at the Zonos-v0.1-hybrid dims), K / V of the attention
+layers only.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN
+from .engine import HEADS_N, HEADS_N_PAD, HipEngine
+
+
+def rope_table_neox(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
+    """flash-attn RotaryEmbedding cache (mamba_ssm MHA, rotary_emb_dim = head dim): fp32 angles, cos / sin
+    cast to bf16 (the activation dtype), stored as fp32 (cos, sin) pairs for the QKV epilogue."""
+    inv = 1.0 / (10000.0 ** (torch.arange(0, hd, 2, dtype=torch.float32) / hd))
+    ang = torch.outer(torch.arange(n, dtype=torch.float32), inv)
+    return torch.stack([torch.cos(ang).bfloat16().float(), torch.sin(ang).bfloat16().float()], dim=-1).contiguous()
+
+
+def neox_pair_perm(hd: int) -> torch.Tensor:
+    """Row order putting element j next to j + hd/2 (the halves the non-interleaved rotary pairs), so the
+    interleaved-pair RoPE epilogue applies it. q and k both carry it, so q.k is unchanged."""
+    j = torch.arange(hd // 2)
+    return torch.stack([j, j + hd // 2], dim=1).flatten()
+
+
+class HybridEngine(HipEngine):
+    hybrid = True
+
+    def __init__(self, cfg, device="cuda", max_slots: int = 1, max_seqlen: int = 2048, max_prefill: int = 512):
+        bb = cfg.backbone
+        if bb.rms_norm or bb.residual_in_fp32:
+            raise NotImplementedError("hybrid blocks are built for LayerNorm with bf16 residuals (Zonos-v0.1-hybrid)")
+        self.md = bb.mamba2_dims()
+        md = self.md
+        if (md["headdim"], md["d_state"], md["d_conv"], md["ngroups"]) != (64, 128, 4, 1) or not md["rmsnorm"] \
+                or md["norm_before_gate"] or md["D_has_hdim"]:
+            raise NotImplementedError(f"Mamba2 geometry not built: {md}")
+        self.attn_idx = sorted(int(i) for i in bb.attn_layer_idx)
+        self.Fm = int(bb.d_intermediate)
+        super().__init__(cfg, device, max_slots, max_seqlen, max_prefill)
+        self.attn_block = False  # the fused QKV + attention launch needs the LayerNorm prologue
+
+    def _kv_layers(self) -> int:
+        return len(self.attn_idx)
+
+    def _alloc(self):
+        super()._alloc()
+        md, R, P, dev = self.md, self.R, self.max_prefill, self.dev
+        nm = self.L - len(self.attn_idx)
+        z = lambda *shape, dt=torch.bfloat16: torch.zeros(*shape, dtype=dt, device=dev)  # noqa: E731
+        with torch.cuda.stream(self.stream):
+            self.hid, self.nrm = z(R, self.d), z(R, self.d)
+            self.zx, self.yb, self.yn = z(R, md["d_in_proj"]), z(R, md["d_ssm"]), z(R, md["d_ssm"])
+            self.hid_pre, self.nrm_pre = z(2 * P, self.d), z(2 * P, self.d)
+            self.zx_pre, self.yb_pre, self.yn_pre = z(2 * P, md["d_in_proj"]), z(2 * P, md["d_ssm"]), z(2 * P, md["d_ssm"])
+            self.hm = z(R, max(self.Fm, self.F, 1))
+            self.hm_pre = z(2 * P, max(self.Fm, self.F, 1))
+            self.conv_ring = z(nm, R, md["d_conv"], md["conv_dim"])
+            self.ssm = z(nm, R, md["nheads"], md["headdim"], md["d_state"])
+            self.rope = rope_table_neox(self.hd).to(dev)
+        self.stream.synchronize()
+
+    # ------------------------------------------------------------------ weights
+    def load_state_dict(self, sd: dict):
+        """mamba-ssm parameter names (Block norm / mixer / norm2 / mlp; Mamba2, MHA, GatedMLP)."""
+        bf = lambda t: t.to(self.dev, torch.bfloat16).contiguous()  # noqa: E731
+        f32 = lambda t: t.to(self.dev, torch.bfloat16).float().contiguous()  # noqa: E731  (bf16 model params)
+        md, hd = self.md, self.hd
+        perm = neox_pair_perm(hd)
+        with torch.cuda.stream(self.stream):
+            w = {}
+            if "embeddings.0.weight" in sd:
+                w["emb"] = torch.stack([bf(sd[f"embeddings.{k}.weight"])[:EMB_VOCAB] for k in range(N_CODEBOOKS)])
+            layers = []
+            for i in range(self.L):
+                p = f"backbone.layers.{i}."
+                lw = dict(ln1_w=bf(sd[p + "norm.weight"]), ln1_b=bf(sd[p + "norm.bias"]))
+                if i in self.attn_idx:
+                    qkv = bf(sd[p + "mixer.in_proj.weight"])
+                    nq, nk = self.H * hd, self.Hkv * hd
+                    q = qkv[:nq].view(self.H, hd, -1)[:, perm.to(self.dev)].reshape(nq, -1)
+                    k = qkv[nq:nq + nk].view(self.Hkv, hd, -1)[:, perm.to(self.dev)].reshape(nk, -1)
+                    lw.update(kind="attn", kv=self.attn_idx.index(i),
+                              qkv=self._pack(torch.cat([q, k, qkv[nq + nk:]]), nq + 2 * nk),
+                              out=self._pack(sd[p + "mixer.out_proj.weight"], self.d))
+                    ff = self.F
+                else:
+                    lw.update(kind="mamba", st=i - sum(1 for j in self.attn_idx if j < i),
+                              in_proj=self._pack(sd[p + "mixer.in_proj.weight"], md["d_in_proj"]),
+                              conv_w=bf(sd[p + "mixer.conv1d.weight"]).reshape(md["conv_dim"], md["d_conv"]).contiguous(),
+                              conv_b=bf(sd[p + "mixer.conv1d.bias"]),
+                              dt_bias=f32(sd[p + "mixer.dt_bias"]),
+                              A=(-torch.exp(f32(sd[p + "mixer.A_log"]))).contiguous(),
+                              D=f32(sd[p + "mixer.D"]),
+                              norm_w=bf(sd[p + "mixer.norm.weight"]),
+                              out=self._pack(sd[p + "mixer.out_proj.weight"], self.d))
+                    ff = self.Fm
+                if ff:
+                    lw.update(ff=ff, ln2_w=bf(sd[p + "norm2.weight"]), ln2_b=bf(sd[p + "norm2.bias"]),
+                              fc1=self._pack(sd[p + "mlp.fc1.weight"], 2 * ff, _lib.PACK_SWIGLU),
+                              fc2=self._pack(sd[p + "mlp.fc2.weight"], self.d))
+                layers.append(lw)
+            w["layers"] = layers
+            w["nf_w"], w["nf_b"] = bf(sd["backbone.norm_f.weight"]), bf(sd["backbone.norm_f.bias"])
+            if "heads.0.weight" in sd:
+                heads = torch.zeros(HEADS_N, self.d, dtype=torch.bfloat16, device=self.dev)
+                for k in range(N_CODEBOOKS):
+                    heads[k * 1026: k * 1026 + HEAD_VOCAB] = bf(sd[f"heads.{k}.weight"])[:HEAD_VOCAB]
+                w["heads"] = self._pack(heads, HEADS_N_PAD)
+                del heads
+        self.stream.synchronize()
+        self.w = w
+        self._build_plan()
+
+    # ------------------------------------------------------------------ launch helpers
+    def _addln(self, hid, res, ln, out, m, store=True):
+        lib, d, eps, s = self.lib, self.d, self.eps, self.sptr
+        hp = None if hid is None else hid.data_ptr()
+        rp, wp, bp, op = res.data_ptr(), ln[0].data_ptr(), ln[1].data_ptr(), out.data_ptr()
+        st = 1 if store else 0
+
+        def run():
+            _lib.check(lib.zmi_add_layernorm(hp, d, rp, d, m, d, wp, bp, eps, op, d, st, s), "add_layernorm")
+        return run
+
+    def _mamba_args(self, lw, zx, y, m, row_pos, row_kv) -> _lib.Mamba2Args:
+        md = self.md
+        a = _lib.Mamba2Args()
+        a.zxbcdt, a.ld_zx, a.M = zx.data_ptr(), md["d_in_proj"], m
+        a.d_ssm, a.nheads, a.headdim, a.d_state, a.d_conv, a.ngroups = (md["d_ssm"], md["nheads"], md["headdim"],
+                                                                        md["d_state"], md["d_conv"], md["ngroups"])
+        a.conv_w, a.conv_b = lw["conv_w"].data_ptr(), lw["conv_b"].data_ptr()
+        a.dt_bias, a.A, a.D = lw["dt_bias"].data_ptr(), lw["A"].data_ptr(), lw["D"].data_ptr()
+        a.conv_ring, a.ssm = self.conv_ring[lw["st"]].data_ptr(), self.ssm[lw["st"]].data_ptr()
+        a.y, a.ldy = y.data_ptr(), md["d_ssm"]
+        a.row_pos = row_pos.data_ptr()
+        a.row_kv = _lib.ptr(row_kv)
+        return a
+
+    def _gnorm(self, lw, y, zx, out, m):
+        lib, md, s = self.lib, self.md, self.sptr
+        yp, zp, wp, op = y.data_ptr(), zx.data_ptr(), lw["norm_w"].data_ptr(), out.data_ptr()
+
+        def run():
+            _lib.check(lib.zmi_gated_rmsnorm(yp, md["d_ssm"], zp, md["d_in_proj"], m, md["d_ssm"], wp, 1e-5, op,
+                                             md["d_ssm"], s), "gated_rmsnorm")
+        return run
+
+    def _call_step(self, a):
+        lib, s = self.lib, self.sptr
+
+        def run():
+            _lib.check(lib.zmi_mamba2_step(ctypes.byref(a), s), "mamba2_step")
+        return run
+
+    def _layer_items(self, lw, m, x, hid, nrm, zx, yb, yn, hm, q, attn, row_kv, row_pos, first, seq_len=None,
+                     max_pos=None):
+        """Launches of one block over m rows (decode: seq_len None; prefill: sequences of seq_len rows)."""
+        d, md, qd = self.d, self.md, self.H * self.hd
+        items = [("call", self._addln(None if first else hid, x, (lw["ln1_w"], lw["ln1_b"]), nrm, m))]
+        if lw["kind"] == "attn":
+            j = lw["kv"]
+            qkv_n = (self.H + 2 * self.Hkv) * self.hd
+            items.append(("gemv", self._gemv(lw["qkv"], nrm, m, qkv_n, d, _lib.EPI_QKV, q, qd,
+                                             kv=(self.kc[j], self.vc[j]), row_kv=row_kv, row_pos=row_pos)))
+            if seq_len is None:
+                items.append(("attn", j))
+            else:
+                items.append(("call", lambda j=j: self._attention(j, q, m, row_kv, row_pos, max_pos, attn)))
+            items.append(("gemv", self._gemv(lw["out"], attn, m, d, qd, _lib.EPI_STORE, hid, d)))
+        else:
+            items.append(("gemv", self._gemv(lw["in_proj"], nrm, m, md["d_in_proj"], d, _lib.EPI_STORE, zx,
+                                             md["d_in_proj"])))
+            if seq_len is None:
+                items.append(("call", self._call_step(self._mamba_args(lw, zx, yb, m, row_pos, None))))
+            else:
+                a = self._mamba_args(lw, zx, yb, m, row_pos, row_kv)
+                lib, s = self.lib, self.sptr
+                items.append(("call", lambda a=a: _lib.check(lib.zmi_mamba2_scan(ctypes.byref(a), seq_len, s),
+                                                             "mamba2_scan")))
+            items.append(("call", self._gnorm(lw, yb, zx, yn, m)))
+            items.append(("gemv", self._gemv(lw["out"], yn, m, d, md["d_ssm"], _lib.EPI_STORE, hid, d)))
+        if lw.get("ff"):
+            ff = lw["ff"]
+            items.append(("call", self._addln(hid, x, (lw["ln2_w"], lw["ln2_b"]), nrm, m)))
+            items.append(("gemv", self._gemv(lw["fc1"], nrm, m, 2 * ff, d, _lib.EPI_SWIGLU, hm, ff)))
+            items.append(("gemv", self._gemv(lw["fc2"], hm, m, d, ff, _lib.EPI_STORE, hid, d)))
+        return items
+
+    # ------------------------------------------------------------------ decode plan
+    def _plan(self, rows: int) -> list:
+        if rows not in self._plans:
+            w = self.w
+            plan = []
+            for i, lw in enumerate(w["layers"]):
+                plan += self._layer_items(lw, rows, self.x, self.hid, self.nrm, self.zx, self.yb, self.yn, self.hm,
+                                          self.q, self.attn, self.row_kv, self.row_pos, first=(i == 0))
+            plan.append(("call", self._addln(self.hid, self.x, (w["nf_w"], w["nf_b"]), self.nrm, rows, store=False)))
+            plan.append(("gemv", self._gemv(w["heads"], self.nrm, rows, HEADS_N_PAD, self.d, _lib.EPI_LOGITS,
+                                            self.logits, 0, n_valid=HEADS_N)))
+            self._plans[rows] = plan
+        return self._plans[rows]
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill_layers(self, m: int, max_pos: int):
+        """m rows = sequences of max_pos + 1 rows each, every sequence from position 0 (Mamba2.forward
+        from an empty cache; the reference's step() takes one token at a time after that)."""
+        seq_len = max_pos + 1
+        if m % seq_len:
+            raise ValueError("hybrid prefill: rows must be whole sequences starting at position 0")
+        for i, lw in enumerate(self.w["layers"]):
+            for kind, item in self._layer_items(lw, m, self.x_pre, self.hid_pre, self.nrm_pre, self.zx_pre,
+                                                self.yb_pre, self.yn_pre, self.hm_pre, self.q_pre, self.attn_pre,
+                                                self.row_kv_pre, self.row_pos_pre, first=(i == 0), seq_len=seq_len,
+                                                max_pos=max_pos):
+                if kind == "gemv":
+                    self._run_gemv(item)
+                else:
+                    item()
+
+    def _prefill_logits(self, s_len: int):
+        d = self.d
+        off = (s_len - 1) * d * 2  # bytes: row s_len - 1, then the uncond row s_len further on
+        lib = self.lib
+        _lib.check(lib.zmi_add_layernorm(self.hid_pre.data_ptr() + off, s_len * d, self.x_pre.data_ptr() + off,
+                                         s_len * d, 2, d, self.w["nf_w"].data_ptr(), self.w["nf_b"].data_ptr(),
+                                         self.eps, self.x_last.data_ptr(), d, 0, self.sptr), "norm_f")
+        self._run_gemv(self._gemv(self.w["heads"], self.x_last, 2, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits_pre,
+                                  0, n_valid=HEADS_N))
+
+    def final_norm_pre(self, m: int, out: torch.Tensor):
+        _lib.check(self.lib.zmi_add_layernorm(self.hid_pre.data_ptr(), self.d, self.x_pre.data_ptr(), self.d, m,
+                                              self.d, self.w["nf_w"].data_ptr(), self.w["nf_b"].data_ptr(), self.eps,
+                                              out.data_ptr(), self.d, 0, self.sptr), "norm_f")
+
+    def inference_cache(self) -> dict:
+        """{layer: (K, V^T)} for MHA layers, {layer: (conv ring, ssm state)} for Mamba2 layers."""
+        out = {}
+        for i, lw in enumerate(self.w["layers"]):
+            if lw["kind"] == "attn":
+                out[i] = (self.kc[lw["kv"]], self.vc[lw["kv"]])
+            else:
+                out[i] = (self.conv_ring[lw["st"]], self.ssm[lw["st"]])
+        return out

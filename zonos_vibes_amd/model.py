@@ -19,7 +19,7 @@ from . import _lib  # noqa: F401  (fail loudly at import if the HIP library is m
 from .autoencoder import DACAutoencoder
 from .conditioning import PrefixConditioner
 from .config import N_CODEBOOKS, ZonosConfig
-from .engine import HipEngine, SamplingParams
+from .engine import SamplingParams, make_engine
 
 
 def _draw_seed() -> int:
@@ -35,7 +35,7 @@ class Zonos:
         self.eos_token_id = config.eos_token_id
         self.masked_token_id = config.masked_token_id
         self._device = torch.device(device)
-        self.engine = HipEngine(config, device, max_slots, max_seqlen, max_prefill)
+        self.engine = make_engine(config, device, max_slots, max_seqlen, max_prefill)
         self.autoencoder = autoencoder if autoencoder is not None else DACAutoencoder(device)
         pcc = config.prefix_conditioner
         self.prefix_conditioner = (PrefixConditioner(pcc.conditioners, config.backbone.d_model, device, pcc.projection)
@@ -59,7 +59,8 @@ class Zonos:
         """model.py:65-88 with local files only (safetensors, no pickle)."""
         from safetensors.torch import load_file
         if backbone not in (None, "hip"):
-            raise ValueError(f"backbone {backbone!r}: only the 'hip' transformer backbone is built")
+            raise ValueError(f"backbone {backbone!r}: the HIP build registers BACKBONES['hip'] only "
+                             "(transformer and hybrid)")
         config = ZonosConfig.from_dict(json.load(open(config_path)))
         dac = DACAutoencoder(device, state_dict=load_file(dac_path) if dac_path else None)
         m = cls(config, device, autoencoder=dac, **kw)
@@ -81,8 +82,8 @@ class Zonos:
         e = self.engine
         if slots > e.S or seqlen > e.smax or prefill > e.max_prefill:
             w = e.w
-            self.engine = HipEngine(self.config, self._device, max(slots, e.S), max(seqlen, e.smax),
-                                    max(prefill, e.max_prefill))
+            self.engine = make_engine(self.config, self._device, max(slots, e.S), max(seqlen, e.smax),
+                                      max(prefill, e.max_prefill))
             self.engine.w = w
             self.engine._build_plan()
 
@@ -196,7 +197,8 @@ class Zonos:
 
     def __repr__(self):
         bb = self.config.backbone
-        return f"Zonos(hip, d={bb.d_model}, layers={bb.n_layer}, heads={bb.num_heads}/{bb.num_heads_kv})"
+        kind = "hybrid" if bb.is_hybrid else "transformer"
+        return f"Zonos(hip {kind}, d={bb.d_model}, layers={bb.n_layer}, heads={bb.num_heads}/{bb.num_heads_kv})"
 
 
 __all__ = ["Zonos", "DACAutoencoder", "N_CODEBOOKS"]

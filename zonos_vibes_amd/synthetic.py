@@ -100,8 +100,10 @@ W_STD = 0.02
 
 
 def zonos_specs(cfg: ZonosConfig) -> list[Spec]:
-    """bf16 tensors of the transformer Zonos model (un-padded reference shapes)."""
+    """bf16 tensors of the Zonos model (un-padded reference shapes)."""
     bb = cfg.backbone
+    if bb.is_hybrid:
+        return hybrid_specs(cfg)
     d, hd = bb.d_model, bb.head_dim
     a = W_STD * SQRT3
     qkv = (bb.num_heads + 2 * bb.num_heads_kv) * hd
@@ -125,6 +127,42 @@ def zonos_specs(cfg: ZonosConfig) -> list[Spec]:
             Spec("backbone.norm_f.bias", (d,), "bf16", 0.02)]
     for k in range(N_CODEBOOKS):
         out.append(Spec(f"heads.{k}.weight", (HEAD_VOCAB, d), "bf16", a))
+    return out
+
+
+def hybrid_specs(cfg: ZonosConfig) -> list[Spec]:
+    """bf16 tensors of the hybrid model, mamba-ssm parameter names (Block: norm, mixer, norm2, mlp;
+    Mamba2: in_proj, conv1d, dt_bias, A_log, D, norm, out_proj; MHA: in_proj, out_proj; GatedMLP: fc1,
+    fc2). Init ranges follow Mamba2's: A = -exp(A_log) in [-16, -1]; dt = softplus(dt_bias + ..) around
+    0.05-0.3 so the state carries several steps; D near 1."""
+    bb = cfg.backbone
+    d, a = bb.d_model, W_STD * SQRT3
+    md = bb.mamba2_dims()
+    out = [Spec(f"embeddings.{k}.weight", (EMB_VOCAB, d), "bf16", a) for k in range(N_CODEBOOKS)]
+    for i in range(bb.n_layer):
+        p = f"backbone.layers.{i}."
+        out += [Spec(p + "norm.weight", (d,), "bf16", 0.1, 1.0), Spec(p + "norm.bias", (d,), "bf16", 0.02)]
+        if i in bb.attn_layer_idx:
+            hd = bb.head_dim
+            out += [Spec(p + "mixer.in_proj.weight", ((bb.num_heads + 2 * bb.num_heads_kv) * hd, d), "bf16", a),
+                    Spec(p + "mixer.out_proj.weight", (d, bb.num_heads * hd), "bf16", a)]
+            ff = bb.attn_mlp_d_intermediate
+        else:
+            out += [Spec(p + "mixer.in_proj.weight", (md["d_in_proj"], d), "bf16", a),
+                    Spec(p + "mixer.conv1d.weight", (md["conv_dim"], 1, md["d_conv"]), "bf16", 0.5),
+                    Spec(p + "mixer.conv1d.bias", (md["conv_dim"],), "bf16", 0.1),
+                    Spec(p + "mixer.dt_bias", (md["nheads"],), "bf16", 1.0, -2.0),
+                    Spec(p + "mixer.A_log", (md["nheads"],), "bf16", 1.386, 1.386),
+                    Spec(p + "mixer.D", (md["nheads"],), "bf16", 0.1, 1.0),
+                    Spec(p + "mixer.norm.weight", (md["d_ssm"],), "bf16", 0.1, 1.0),
+                    Spec(p + "mixer.out_proj.weight", (d, md["d_ssm"]), "bf16", W_STD * SQRT3)]
+            ff = bb.d_intermediate
+        if ff:
+            out += [Spec(p + "norm2.weight", (d,), "bf16", 0.1, 1.0), Spec(p + "norm2.bias", (d,), "bf16", 0.02),
+                    Spec(p + "mlp.fc1.weight", (2 * ff, d), "bf16", a), Spec(p + "mlp.fc2.weight", (d, ff), "bf16", a)]
+    out += [Spec("backbone.norm_f.weight", (d,), "bf16", 0.1, 1.0),
+            Spec("backbone.norm_f.bias", (d,), "bf16", 0.02)]
+    out += [Spec(f"heads.{k}.weight", (HEAD_VOCAB, d), "bf16", a) for k in range(N_CODEBOOKS)]
     return out
 
 
