@@ -201,6 +201,70 @@ def step_bytes(model, pos: int) -> int:
     return w + kv
 
 
+def hybrid_step_bytes(e, pos: int) -> int:
+    """Algorithmic HBM bytes of one hybrid decode step (2 CFG rows): every weight once, each Mamba2 layer's
+    SSM state read + written (2 rows x nheads x 64 x 128 bf16) and conv ring slot traffic, the attention
+    layers' K / V up to pos."""
+    md, d = e.md, e.d
+    n_attn = len(e.attn_idx)
+    n_mamba = e.L - n_attn
+    qkv = (e.H + 2 * e.Hkv) * e.hd
+    w_m = md["d_in_proj"] * d + d * md["d_ssm"] + md["conv_dim"] * (md["d_conv"] + 1) + md["d_ssm"]
+    w_a = qkv * d + d * e.H * e.hd
+    w = 2 * (n_mamba * w_m + n_attn * w_a + e.L * 2 * d) + 9 * 1025 * d * 2
+    state = n_mamba * 2 * (2 * md["nheads"] * md["headdim"] * md["d_state"] * 2 + 4 * md["conv_dim"] * 2)
+    kv = n_attn * 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)
+    return w + state + kv
+
+
+def time_hybrid(dev, n_new: int) -> dict:
+    """BASELINE config C4 (Zonos-v0.1-hybrid, batch 1, one GPU): one C2-shaped utterance (Lc 160, n_new
+    frames, greedy, EOS suppressed) through generate() + DAC decode, wall-clock RTF, and the decode step
+    at the utterance's mean position (HIP events) against the step's algorithmic HBM bytes."""
+    from zonos_vibes_amd.config import zonos_v01_hybrid
+    from zonos_vibes_amd.engine import SamplingParams
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_hybrid()
+    m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n_new + 9, max_prefill=LC + 1)
+    cond = cond_tensor(1, cfg.backbone.d_model, dev)
+
+    def one():
+        codes = m.generate(cond, max_new_tokens=n_new, sampling_params=dict(temperature=0.0), progress_bar=False,
+                           chunk=128)
+        return codes, m.autoencoder.decode(codes)
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes, wav = one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    assert codes.shape[-1] == n_new
+    e = m.engine
+    s_len = e.prefill(0, cond, None, n_new, SamplingParams(temperature=0.0))
+    lead, steps = max(0, n_new // 2 - 32), 64
+    e.step(lead, slots=1)
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(e.stream):
+        st.record(e.stream)
+        e.step(steps, slots=1)
+        en.record(e.stream)
+    en.synchronize()
+    e.release(0)
+    us = st.elapsed_time(en) * 1000.0 / steps
+    pos = s_len + lead + steps // 2
+    b = hybrid_step_bytes(e, pos)
+    out = {"config": f"C4: Zonos-v0.1-hybrid dims (46 layers: 41 Mamba2 + MHA at 9/18/27/36/45), batch 1, Lc={LC}, "
+                     f"{n_new} frames, greedy, EOS suppressed, + DAC decode",
+           "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3), "utterance_ms": round(el * 1e3, 1),
+           "decode_step_us": round(us, 1), "decode_step_pos": pos, "step_bytes": b,
+           "decode_step_hbm_frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
+           "parity": "unpinned (mamba-ssm absent); held to oracle/hybrid_cpu.py by tests/test_gpu_hybrid.py"}
+    del m, e
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_cores() -> int:
     """CPU threads available to this process: its affinity set, capped by OMP_NUM_THREADS when the host
     sets one (the GPU box gives each GPU a 16-thread share and sets OMP_NUM_THREADS=16)."""
@@ -267,6 +331,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--new-tokens", type=int, default=N_NEW)
+    ap.add_argument("--no-hybrid", action="store_true", help="skip the C4 hybrid-backbone line in `widened`")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -337,6 +402,8 @@ def main():
     us, bl = time_dominant_kernel(model)
     step_us, step_pos = time_decode_step(model, cond)
     widened = time_widened_rows(model, dev)
+    if rank == 0 and not args.no_hybrid:
+        widened["hybrid_c4"] = time_hybrid(dev, n_new)
     breakdown = utterance_breakdown(model, cond, n_new)
     out = None
     if rank == 0:

@@ -64,6 +64,12 @@ __global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args 
   const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
   __shared__ float xs[MB_HD], bc[2 * MB_DS];
   const int t = threadIdx.x;
+  // the state slice first: its 64 B per lane are the longest loads, in flight under the conv phase
+  const int p = t >> 2, nq = t & 3;
+  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
+  uint4 sv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sv[j] = reinterpret_cast<const uint4*>(st)[j];
 
   // (1) conv + SiLU of this head's 64 x channels and the 256 B / C channels (every head recomputes
   // B / C; head 0 alone writes their ring slot)
@@ -86,11 +92,6 @@ __global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args 
   __syncthreads();
 
   // (3) state update and readout: lane (p, quarter) owns state[p][32 quarter .. +31]
-  const int p = t >> 2, nq = t & 3;
-  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
-  uint4 sv[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) sv[j] = reinterpret_cast<const uint4*>(st)[j];
   const float x = xs[p];
   const float* B = bc + nq * 32;
   const float* C = bc + MB_DS + nq * 32;
@@ -194,22 +195,45 @@ __global__ __launch_bounds__(MB_NT) void mamba2_scan_kernel(const ZmiMamba2Args 
   }
 }
 
+// Row reductions of the two norms below: one 256-thread workgroup per row; the row is cut into NW
+// contiguous parts (4, or K / 512 below K = 2048), wave w < NW owns part w, lane L its 8-element chunks
+// L + 64 i; fp32 sums in chunk order, DPP wave sums, parts combined as (p0 + p1) + (p2 + p3) (absent parts
+// add +0, exactly). A row's bits do not depend on M.
+template <int K>
+struct RowSplit {
+  static constexpr int NW = K >= 2048 ? 4 : K / 512;
+  static constexpr int CPL = K / (512 * NW);
+  static_assert(NW >= 1 && CPL >= 1 && NW * CPL * 512 == K, "row split");
+};
+__device__ __forceinline__ float block_sum4(float v, float* part) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();  // part[] may still be read by the previous reduction
+  if ((threadIdx.x & 63) == 0) part[wave] = v;
+  __syncthreads();
+  return (part[0] + part[1]) + (part[2] + part[3]);
+}
+
 // ---------------------------------------------------------------------------- add + LayerNorm
 // layer_norm_fn(x, w, b, residual, prenorm=True, residual_in_fp32=False) (mamba_ssm/ops/triton/
 // layer_norm.py): s = x + residual in fp32; residual_out = bf16(s); y = (s - mean) * rstd * w + b on the
-// fp32 sum (two-pass statistics). One wave per row, lane L owns the 8-element chunks 8 (L + 64 i).
-template <int CPL>
-__global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh, bf16_t* res, int ldr, int m,
+// fp32 sum (two-pass statistics).
+template <int K>
+__global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh, bf16_t* res, int ldr,
                                                      const bf16_t* w, const bf16_t* b, float eps, bf16_t* out, int ldo,
                                                      int store_res) {
-  constexpr int K = CPL * 512;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= m) return;
+  constexpr int NW = RowSplit<K>::NW, CPL = RowSplit<K>::CPL;
+  __shared__ float part[4];
+  const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool on = wave < NW;
   float v[CPL][8];
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    if (!on) continue;
+    const int c = wave * (K / (8 * NW)) + lane + 64 * i;  // 8-element chunk index in the row
     const uint4 rv = reinterpret_cast<const uint4*>(res + (size_t)r * ldr)[c];
     uint32_t u[4] = {rv.x, rv.y, rv.z, rv.w};
     uint32_t hu[4] = {0u, 0u, 0u, 0u};
@@ -229,19 +253,20 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh,
       reinterpret_cast<uint4*>(res + (size_t)r * ldr)[c] = uint4{u[0], u[1], u[2], u[3]};
     }
   }
-  const float mean = wave_sum(sum) / (float)K;
+  const float mean = block_sum4(sum, part) / (float)K;
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float d = v[i][e] - mean;
-      sq += d * d;
+      sq += on ? d * d : 0.f;
     }
-  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + eps);
+  const float rstd = 1.0f / sqrtf(block_sum4(sq, part) / (float)K + eps);
+  if (!on) return;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+    const int c = wave * (K / (8 * NW)) + lane + 64 * i;
     const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
     const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gb.x, gb.y, gb.z, gb.w};
     uint32_t o[4];
@@ -258,18 +283,21 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh,
 // ---------------------------------------------------------------------------- gated RMSNorm
 // RMSNormGated(norm_before_gate=False, one group) (mamba_ssm/ops/triton/layernorm_gated.py):
 // g = y * (z * sigmoid(z)) in fp32, out = g * rstd * w with rstd = 1 / sqrt(mean(g^2) + eps), bf16.
-// One wave per row, lane L owns the 8-element chunks 8 (L + 64 i).
-template <int CPL>
-__global__ __launch_bounds__(256) void gated_rms_kernel(const bf16_t* y, int ldy, const bf16_t* z, int ldz, int m,
+template <int K>
+__global__ __launch_bounds__(256) void gated_rms_kernel(const bf16_t* y, int ldy, const bf16_t* z, int ldz,
                                                         const bf16_t* w, float eps, bf16_t* out, int ldo) {
-  constexpr int K = CPL * 512;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= m) return;
+  constexpr int NW = RowSplit<K>::NW, CPL = RowSplit<K>::CPL;
+  __shared__ float part[4];
+  const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool on = wave < NW;
   float g[CPL][8];
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[i][e] = 0.f;
+    if (!on) continue;
+    const int c = wave * (K / (8 * NW)) + lane + 64 * i;
     const uint4 yv = reinterpret_cast<const uint4*>(y + (size_t)r * ldy)[c];
     const uint4 zv = reinterpret_cast<const uint4*>(z + (size_t)r * ldz)[c];
     const uint32_t uy[4] = {yv.x, yv.y, yv.z, yv.w}, uz[4] = {zv.x, zv.y, zv.z, zv.w};
@@ -281,10 +309,11 @@ __global__ __launch_bounds__(256) void gated_rms_kernel(const bf16_t* y, int ldy
       sq += g[i][e] * g[i][e];
     }
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + eps);
+  const float rstd = 1.0f / sqrtf(block_sum4(sq, part) / (float)K + eps);
+  if (!on) return;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
-    const int c = lane + 64 * i;
+    const int c = wave * (K / (8 * NW)) + lane + 64 * i;
     const uint4 gw = reinterpret_cast<const uint4*>(w)[c];
     const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
     uint32_t o[4];
@@ -331,16 +360,16 @@ extern "C" int zmi_add_layernorm(const void* hidden, int ldh, void* residual, in
   if (ldh % 8 || ldr % 8 || ldo % 8) return zmi_fail_msg("add_layernorm: leading dimensions must be multiples of 8");
   if (!residual || !w || !b || !out) return zmi_fail_msg("add_layernorm: missing buffers");
   if (m <= 0) return 0;
-  const dim3 grid((m + 3) / 4);
+  const dim3 grid((unsigned)m);
   hipStream_t s = (hipStream_t)stream;
-#define ZMI_ADDLN(CPL)                                                                                         \
-  hipLaunchKernelGGL(add_ln_kernel<CPL>, grid, dim3(256), 0, s, (const bf16_t*)hidden, ldh, (bf16_t*)residual, \
-                     ldr, m, (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo, store_residual)
+#define ZMI_ADDLN(KK)                                                                                         \
+  hipLaunchKernelGGL(add_ln_kernel<KK>, grid, dim3(256), 0, s, (const bf16_t*)hidden, ldh, (bf16_t*)residual, \
+                     ldr, (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)out, ldo, store_residual)
   switch (k) {
-    case 512: ZMI_ADDLN(1); break;
-    case 1024: ZMI_ADDLN(2); break;
-    case 2048: ZMI_ADDLN(4); break;
-    case 4096: ZMI_ADDLN(8); break;
+    case 512: ZMI_ADDLN(512); break;
+    case 1024: ZMI_ADDLN(1024); break;
+    case 2048: ZMI_ADDLN(2048); break;
+    case 4096: ZMI_ADDLN(4096); break;
     default: return zmi_fail_msg("add_layernorm: k must be 512, 1024, 2048 or 4096");
   }
 #undef ZMI_ADDLN
@@ -354,14 +383,14 @@ extern "C" int zmi_gated_rmsnorm(const void* y, int ldy, const void* z, int ldz,
   if (!y || !z || !w || !out) return zmi_fail_msg("gated_rmsnorm: missing buffers");
   if (m <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-#define ZMI_GRMS(CPL)                                                                                          \
-  hipLaunchKernelGGL(gated_rms_kernel<CPL>, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, (const bf16_t*)y, ldy, \
-                     (const bf16_t*)z, ldz, m, (const bf16_t*)w, eps, (bf16_t*)out, ldo)
+#define ZMI_GRMS(KK)                                                                                          \
+  hipLaunchKernelGGL(gated_rms_kernel<KK>, dim3((unsigned)m), dim3(256), 0, s, (const bf16_t*)y, ldy,         \
+                     (const bf16_t*)z, ldz, (const bf16_t*)w, eps, (bf16_t*)out, ldo)
   switch (k) {
-    case 512: ZMI_GRMS(1); break;
-    case 1024: ZMI_GRMS(2); break;
-    case 2048: ZMI_GRMS(4); break;
-    case 4096: ZMI_GRMS(8); break;
+    case 512: ZMI_GRMS(512); break;
+    case 1024: ZMI_GRMS(1024); break;
+    case 2048: ZMI_GRMS(2048); break;
+    case 4096: ZMI_GRMS(4096); break;
     default: return zmi_fail_msg("gated_rmsnorm: k must be 512, 1024, 2048 or 4096");
   }
 #undef ZMI_GRMS
