@@ -100,6 +100,18 @@ int zmi_attention_max_keys_whole(void);
 int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                    void* stream);
 int64_t zmi_attn_block_gran_words(int rows, int hkv);
+/* zmi_attn_block plus `blocks` prefetch-only workgroups that read ptr[0..1][0 .. bytes) once during the
+ * attention phase (HBM is nearly idle there): the next launches' weights (out_proj, the head of fc1) are
+ * then served from the Infinity Cache. Results are those of zmi_attn_block; `sink` is a scratch word the
+ * prefetch may write (never read). */
+typedef struct ZmiPrefetch {
+  const void* ptr[2];
+  int64_t bytes[2];
+  unsigned* sink;
+  int blocks, reserved;
+} ZmiPrefetch;
+int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                      const ZmiPrefetch* prefetch, void* stream);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);

@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
 mkdir -p gpurun_out/keep
 K=gpurun_out/keep
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- \
-  python bench.py --no-cpu-baseline > $K/prof_bench.log 2>&1 || exit $?
+  python bench.py --no-cpu-baseline --no-hybrid > $K/prof_bench.log 2>&1 || exit $?
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} $K/bench_kernel_stats.csv \;
 rm -rf gpurun_out/prof
 pmc() {  # counter, driver, kernel substring, algorithmic bytes, tag

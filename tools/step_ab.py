@@ -16,7 +16,10 @@ import bench  # noqa: E402
 from zonos_vibes_amd.config import zonos_v01_transformer  # noqa: E402
 from zonos_vibes_amd.model import Zonos  # noqa: E402
 
-OPTIONS = [dict(attn_block=False), dict(attn_block=True, attn_block_slices=4), dict(attn_block=True, attn_block_slices=8)]
+OPTIONS = [dict(prefetch_blocks=0), dict(prefetch_blocks=192, prefetch_fc1_mb=0),
+           dict(prefetch_blocks=192, prefetch_fc1_mb=16), dict(prefetch_blocks=192, prefetch_fc1_mb=32),
+           dict(prefetch_blocks=192, prefetch_fc1_mb=64), dict(prefetch_blocks=96, prefetch_fc1_mb=32),
+           dict(prefetch_blocks=0)]
 
 
 def main():

@@ -34,6 +34,11 @@ class GemvArgs(ctypes.Structure):
     ]
 
 
+class Prefetch(ctypes.Structure):
+    _fields_ = [("ptr", c_void_p * 2), ("bytes", c_int64 * 2), ("sink", c_void_p), ("blocks", c_int),
+                ("reserved", c_int)]
+
+
 class Sampling(ctypes.Structure):
     _fields_ = [
         ("temperature", c_float), ("top_p", c_float), ("min_p", c_float), ("linear", c_float),
@@ -86,6 +91,8 @@ _SIGS = {
     "zmi_attention_max_keys_whole": (c_int, []),
     "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
+    "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                  ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_chunk": (c_int, []),

@@ -436,21 +436,50 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   ZMI_ASTAMP(6);
 }
 
+// Prefetch role (optional): while the attention runs, HBM is nearly idle for several microseconds; these
+// workgroups (dispatched on the CUs the projection vacates) read the next launches' weights (out_proj,
+// the head of fc1) once with default-policy loads, so those launches find them in the Infinity Cache.
+// Nothing waits on them and nothing they read is written in this launch.
+__device__ __forceinline__ void prefetch_body(const ZmiPrefetch& pf, int j, int n_pf) {
+  unsigned acc = 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const uint4* p = reinterpret_cast<const uint4*>(pf.ptr[r]);
+    const int64_t nvec = pf.bytes[r] / 16;
+    const int64_t per = (nvec + n_pf - 1) / n_pf;
+    const int64_t lo = (int64_t)j * per, hi = min(lo + per, nvec);
+    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * NT) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t i = i0 + (int64_t)u * NT;
+        v[u] = i < hi ? p[i] : uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  if (acc == 0x9E3779B9u && pf.sink) *pf.sink = acc;  // keeps the loads; the sink is never read
+}
+
 template <int S>
 __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
-                                                        int n_units, uint64_t* gran) {
+                                                        int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
+  const int n_xs = (n_units + 7) / 8 * 8 * S;
   if (b < n_qkv)
     zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_LN, ZMI_EPI_QKV, 1, 1>(
         qa, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, GRAN_STRIDE});
-  else
+  else if (b < n_qkv + n_xs)
     xs_body<S>(at, n_units, b - n_qkv, smem, gran);
+  else
+    prefetch_body(pf, b - n_qkv - n_xs, n_pf);
 }
 
 template <int S>
 hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArgs& at, int n_units, uint64_t* gran,
-                        hipStream_t s) {
+                        const ZmiPrefetch& pf, hipStream_t s) {
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
   const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, true), XsImg<S>::BYTES,
@@ -463,8 +492,9 @@ hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArg
     if (attr != hipSuccess) return attr;
   }
   const int n_xs = (n_units + 7) / 8 * 8 * S;
-  hipLaunchKernelGGL(attn_block_kernel<S>, dim3((unsigned)(n_qkv + n_xs)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
-                     n_units, gran);
+  const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
+  hipLaunchKernelGGL(attn_block_kernel<S>, dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
+                     n_units, gran, pf, n_pf);
   return hipGetLastError();
 }
 
@@ -474,8 +504,8 @@ extern "C" int64_t zmi_attn_block_gran_words(int rows, int hkv) {
   return (rows <= 0 || hkv <= 0) ? -1 : (int64_t)rows * hkv * GRAN_STRIDE;
 }
 
-extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
-                              void* stream) {
+extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                                 const ZmiPrefetch* prefetch, void* stream) {
   const ZmiGemvArgs& a = *qkv;
   if (a.K != 2048 || !a.ln_w) return zmi_fail_msg("attn_block: the QKV projection must be LayerNorm'd with K = 2048");
   if (a.M < 1 || a.M > QRT) return zmi_fail_msg("attn_block: 1 <= M <= 16 rows (one row tile)");
@@ -506,13 +536,25 @@ extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err,
   // diagnostic builds (-DZMI_ATTN_STAMPS -DZMI_GEMV_STAMPS): both roles stamp into qkv->diag, indexed
   // by block (tools/attnblk_stamps.py)
   at.stamps = a.diag ? reinterpret_cast<unsigned long long*>(a.diag) + (size_t)a.reserved * 4096 * 8 : nullptr;
+  ZmiPrefetch pf{};
+  if (prefetch) {
+    pf = *prefetch;
+    if (pf.bytes[0] < 0 || pf.bytes[1] < 0 || (pf.bytes[0] && !pf.ptr[0]) || (pf.bytes[1] && !pf.ptr[1]) ||
+        pf.blocks < 0 || pf.blocks > 4096 || ((pf.bytes[0] | pf.bytes[1]) && pf.blocks == 0))
+      return zmi_fail_msg("attn_block: bad prefetch ranges");
+  }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   switch (slices) {
-    case 4: e = launch_block<4>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, s); break;
-    case 8: e = launch_block<8>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, s); break;
+    case 4: e = launch_block<4>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s); break;
+    case 8: e = launch_block<8>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s); break;
     default: return zmi_fail_msg("attn_block: slices must be 4 or 8");
   }
   ZMI_CHECK(e);
   return 0;
+}
+
+extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                              void* stream) {
+  return zmi_attn_block_pf(qkv, gran, err, attn_out, ldo, slices, nullptr, stream);
 }

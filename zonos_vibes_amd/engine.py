@@ -100,6 +100,10 @@ class HipEngine:
         # positions below the whole-query kernel's reach; identical bits either way (speed only)
         self.attn_block = True
         self.attn_block_slices = 8
+        # prefetch-only workgroups in that launch warm the Infinity Cache with out_proj's weights and the
+        # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only)
+        self.prefetch_blocks = 192
+        self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
         self._plans: dict[int, list] = {}
         self._graphs: dict[int, int] = {}
         self.n_kv = self._kv_layers()
@@ -254,7 +258,13 @@ class HipEngine:
                 qkv = self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                  ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
                 if fused:
-                    plan.append(("attnblk", (qkv[0], i)))
+                    pf = _lib.Prefetch()
+                    if self.prefetch_blocks > 0:
+                        pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
+                        pf.ptr[1] = lw["fc1"].data_ptr()
+                        pf.bytes[1] = min(lw["fc1"].numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
+                        pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
+                    plan.append(("attnblk", (qkv[0], i, pf)))
                 else:
                     plan.append(("gemv", qkv))
                     plan.append(("attn", i))
@@ -275,10 +285,10 @@ class HipEngine:
             "attention")
 
     def _run_attn_block(self, item):
-        a, i = item
-        _lib.check(self.lib.zmi_attn_block(ctypes.byref(a), self.blk_gran[i].data_ptr(), self.blk_err.data_ptr(),
-                                           self.attn.data_ptr(), self.H * self.hd, self.attn_block_slices, self.sptr),
-                   "attn_block")
+        a, i, pf = item
+        _lib.check(self.lib.zmi_attn_block_pf(ctypes.byref(a), self.blk_gran[i].data_ptr(), self.blk_err.data_ptr(),
+                                              self.attn.data_ptr(), self.H * self.hd, self.attn_block_slices,
+                                              ctypes.byref(pf), self.sptr), "attn_block")
 
     def check_errors(self):
         """Raise if an attention launch gave up waiting on an in-launch hand-off (bounded spin)."""
