@@ -146,6 +146,7 @@ class HipEngine:
             self.params = z(S * ctypes.sizeof(_lib.Sampling), dt=torch.uint8)
             P = self.max_prefill
             self.x_pre, self.q_pre, self.attn_pre = z(2 * P, d), z(2 * P, qd), z(2 * P, qd)
+            self.xn_pre = z(2 * P, d)  # LayerNorm'd prefill rows
             self.h_pre = z(2 * P, self.F)
             self.row_kv_pre = z(2 * P, dt=torch.int32)
             self.row_pos_pre = z(2 * P, dt=torch.int32)
@@ -416,19 +417,26 @@ class HipEngine:
                                                self.w["nf_b"].data_ptr(), self.eps, out.data_ptr(), self.d, self.sptr),
                    "norm_f")
 
+    def _ln_pre(self, m: int, ln, out: torch.Tensor):
+        """LayerNorm of the m prefill rows once per layer (zmi_layernorm_rows: the GEMV prologue's arithmetic,
+        bit for bit), so the prefill GEMVs' many row-tile x column-block workgroups run without a prologue."""
+        _lib.check(self.lib.zmi_layernorm_rows(self.x_pre.data_ptr(), self.d, m, self.d, ln[0].data_ptr(),
+                                               ln[1].data_ptr(), self.eps, out.data_ptr(), self.d, self.sptr), "ln")
+
     def _prefill_layers(self, m: int, max_pos: int):
         """The m = 2 x S prefill rows through every layer, with the decode step's kernels (same per-row
-        arithmetic; LayerNorm fused as the GEMV prologue)."""
+        arithmetic; each LayerNorm computed once per layer by zmi_layernorm_rows, identical bits)."""
         d, qd = self.d, self.H * self.hd
         qkv_n = (self.H + 2 * self.Hkv) * self.hd
+        xn = self.xn_pre
         for i, lw in enumerate(self.w["layers"]):
-            self._run_gemv(self._gemv(lw["qkv"], self.x_pre, m, qkv_n, d, _lib.EPI_QKV, self.q_pre, qd,
-                                      ln=(lw["ln1_w"], lw["ln1_b"]), kv=(self.kc[i], self.vc[i]),
-                                      row_kv=self.row_kv_pre, row_pos=self.row_pos_pre))
+            self._ln_pre(m, (lw["ln1_w"], lw["ln1_b"]), xn)
+            self._run_gemv(self._gemv(lw["qkv"], xn, m, qkv_n, d, _lib.EPI_QKV, self.q_pre, qd,
+                                      kv=(self.kc[i], self.vc[i]), row_kv=self.row_kv_pre, row_pos=self.row_pos_pre))
             self._attention(i, self.q_pre, m, self.row_kv_pre, self.row_pos_pre, max_pos, self.attn_pre)
             self._run_gemv(self._gemv(lw["out"], self.attn_pre, m, d, qd, _lib.EPI_RESIDUAL, self.x_pre, d))
-            self._run_gemv(self._gemv(lw["fc1"], self.x_pre, m, 2 * self.F, d, _lib.EPI_SWIGLU, self.h_pre, self.F,
-                                      ln=(lw["ln2_w"], lw["ln2_b"])))
+            self._ln_pre(m, (lw["ln2_w"], lw["ln2_b"]), xn)
+            self._run_gemv(self._gemv(lw["fc1"], xn, m, 2 * self.F, d, _lib.EPI_SWIGLU, self.h_pre, self.F))
             self._run_gemv(self._gemv(lw["fc2"], self.h_pre, m, d, self.F, _lib.EPI_RESIDUAL, self.x_pre, d))
 
     # ------------------------------------------------------------------ readback
