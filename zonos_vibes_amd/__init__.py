@@ -6,6 +6,8 @@ Public surface mirrors the reference (BreakTheBeta/Zonos_Vibes):
     apply/revert_delay_pattern    reference zonos/codebook_pattern.py:5-12   (codebook_pattern.py)
     sample_from_logits            reference zonos/sampling.py:117-182        (sampling.py)
     BACKBONES["hip"]              reference zonos/backbone/__init__.py:1-12  (backbone.py)
+Transformer (Zonos-v0.1-transformer) and hybrid (Zonos-v0.1-hybrid: Mamba2 + attention,
+reference zonos/backbone/_mamba_ssm.py:9-57; hybrid.py) backbones.
 """
 from .config import BackboneConfig, InferenceParams, PrefixConditionerConfig, ZonosConfig  # noqa: F401
 
