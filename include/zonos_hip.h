@@ -33,6 +33,14 @@ enum {
   ZMI_EPI_F32 = 5       /* out f32 [M][ldo] raw fp32 sums (tests)                              */
 };
 enum { ZMI_PACK_IDENTITY = 0, ZMI_PACK_SWIGLU = 1 };
+/* prologue of the activation rows (ZmiGemvArgs.pro):
+ *   AUTO   LayerNorm if ln_w, else the rows as they are;
+ *   ADDLN  mamba-ssm layer_norm_fn(X, ln_w, ln_b, residual = aux, prenorm=True): s = X + aux in fp32,
+ *          LayerNorm(s); res_out (may be NULL) <- bf16(s), written by one workgroup per row tile
+ *          (res_out must not alias aux: other workgroups still read aux);
+ *   GRMS   mamba-ssm RMSNormGated(X, z) * ln_w (norm_before_gate=False, one group), aux = the f32 gate
+ *          z * sigmoid(z) (zmi_mamba2_step's gz), at most 4 rows. */
+enum { ZMI_PRO_AUTO = 0, ZMI_PRO_ADDLN = 2, ZMI_PRO_GRMS = 3 };
 
 typedef struct ZmiGemvArgs {
   const void* W;        /* packed weight (zmi_pack_weight, layout M8)                          */
@@ -53,6 +61,10 @@ typedef struct ZmiGemvArgs {
   int smax, hq, hkv, hd;
   const float* rope;    /* [16384][hd/2][2] (cos, sin) fp32 (_torch.py:9-15)                  */
   void* diag;           /* NULL; diagnostic builds only (-DZMI_GEMV_STAMPS): phase stamps       */
+  int pro;              /* ZMI_PRO_*                                                            */
+  int ld_aux;           /* row stride of aux and res_out (elements)                             */
+  const void* aux;      /* ADDLN: bf16 residual rows; GRMS: f32 gate rows z * sigmoid(z)          */
+  void* res_out;        /* ADDLN: bf16 [M][ld_aux] new residual, or NULL                         */
 } ZmiGemvArgs;
 
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
@@ -244,6 +256,7 @@ typedef struct ZmiMamba2Args {
   int ldy, reserved;
   const int* row_pos;   /* [M] position of the row's token (< 0: inactive row; step only)           */
   const int* row_kv;    /* [M] state row of each activation row (NULL: row m)                       */
+  float* gz;            /* step only, optional: f32 [M][ldy] the gate z * sigmoid(z) of RMSNormGated */
 } ZmiMamba2Args;
 /* Decode: causal_conv1d_update + SiLU + selective_state_update(dt_softplus) for one token per row
  * (mamba_ssm/modules/mamba2.py Mamba2.step). */

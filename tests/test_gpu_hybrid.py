@@ -269,3 +269,60 @@ def synthetic_weights_gpu(m):
         out[sp.name] = t
     torch.cuda.synchronize()
     return out
+
+
+@pytest.mark.parametrize("rows", [1, 2, 4, 5, 8])
+def test_norm_prologues_equal_standalone_kernels(rows):
+    """The decode plan's fused prologues give the prefill path's bits: GEMV(ADDLN) == zmi_add_layernorm +
+    plain GEMV (and its residual output); GEMV(GRMS) on the step kernel's y and f32 gate == zmi_gated_rmsnorm
+    (y, z) + plain GEMV (up to 4 rows)."""
+    from tests.test_gpu_kernels import pack, stream_ptr
+    from zonos_vibes_amd.config import zonos_v01_hybrid
+    L, lib = _lib()
+    for kind, K, N in (("addln", 2048, 8512), ("addln", 512, 2320), ("grms", 4096, 2048), ("grms", 1024, 512)):
+        if kind == "grms" and rows > 4:
+            continue
+        Wp, n_pad = pack(_bf(N, K, scale=0.03, seed=90 + K).to(DEV))
+        w, b = (_bf(K, scale=0.1, seed=93) + 1).to(DEV), _bf(K, scale=0.02, seed=94).to(DEV)
+        fused = torch.zeros(rows, n_pad, dtype=torch.bfloat16, device=DEV)
+        plain = torch.zeros_like(fused)
+        nrm = torch.zeros(rows, K, dtype=torch.bfloat16, device=DEV)
+
+        def gemv(X, pro, out, aux=None, ld_aux=0, res_out=None):
+            a = L.GemvArgs()
+            a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), X.data_ptr(), rows, n_pad, K, K
+            a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), n_pad, n_pad, 1e-5
+            if pro:
+                a.pro, a.aux, a.ld_aux, a.res_out = pro, aux.data_ptr(), ld_aux, L.ptr(res_out)
+                a.ln_w = w.data_ptr()
+                a.ln_b = b.data_ptr() if pro == L.PRO_ADDLN else None
+            L.check(lib.zmi_gemv_launch(ctypes.byref(a), L.EPI_STORE, stream_ptr()), kind)
+
+        if kind == "addln":
+            x = _bf(rows, K, scale=1.5, seed=91).to(DEV)
+            aux = _bf(rows, K, scale=2.0, seed=92).to(DEV)
+            r_out = torch.zeros_like(aux)
+            gemv(x, L.PRO_ADDLN, fused, aux, K, r_out)
+            r_ref = aux.clone()
+            L.check(lib.zmi_add_layernorm(x.data_ptr(), K, r_ref.data_ptr(), K, rows, K, w.data_ptr(), b.data_ptr(),
+                                          1e-5, nrm.data_ptr(), K, 1, stream_ptr()))
+        else:  # y and the gate from the Mamba2 step kernel itself
+            md = (zonos_v01_hybrid() if K == 4096 else tiny_hybrid()).backbone.mamba2_dims()
+            cw, cb, dtb, A, D = (t.to(DEV) for t in _mamba_params(md, 95))
+            zx = _bf(rows, md["d_in_proj"], scale=2.0, seed=96).to(DEV)
+            ring = torch.zeros(rows, 4, md["conv_dim"], dtype=torch.bfloat16, device=DEV)
+            ssm = _bf(rows, md["nheads"], 64, 128, scale=0.5, seed=97).to(DEV)
+            y = torch.zeros(rows, K, dtype=torch.bfloat16, device=DEV)
+            gz = torch.zeros(rows, K, dtype=torch.float32, device=DEV)
+            rp = torch.full((rows,), 9, dtype=torch.int32, device=DEV)
+            a = _args(L, md, zx, cw, cb, dtb, A, D, ring, ssm, y, rows, rp)
+            a.gz = gz.data_ptr()
+            L.check(lib.zmi_mamba2_step(ctypes.byref(a), stream_ptr()), "step")
+            gemv(y, L.PRO_GRMS, fused, gz, K)
+            L.check(lib.zmi_gated_rmsnorm(y.data_ptr(), K, zx.data_ptr(), md["d_in_proj"], rows, K, w.data_ptr(), 1e-5,
+                                          nrm.data_ptr(), K, stream_ptr()))
+        gemv(nrm, 0, plain)
+        torch.cuda.synchronize()
+        assert torch.equal(fused, plain), (kind, K)
+        if kind == "addln":
+            assert torch.equal(r_out, r_ref), (kind, K)

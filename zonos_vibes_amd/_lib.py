@@ -18,6 +18,7 @@ c_int_p = ctypes.POINTER(ctypes.c_int)
 
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
+PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
 
 
 class GemvArgs(ctypes.Structure):
@@ -31,6 +32,7 @@ class GemvArgs(ctypes.Structure):
         ("k_cache", c_void_p), ("v_cache", c_void_p),
         ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
         ("rope", c_void_p), ("diag", c_void_p),
+        ("pro", c_int), ("ld_aux", c_int), ("aux", c_void_p), ("res_out", c_void_p),
     ]
 
 
@@ -71,7 +73,7 @@ class Mamba2Args(ctypes.Structure):
         ("ngroups", c_int),
         ("conv_w", c_void_p), ("conv_b", c_void_p), ("dt_bias", c_void_p), ("A", c_void_p), ("D", c_void_p),
         ("conv_ring", c_void_p), ("ssm", c_void_p), ("y", c_void_p), ("ldy", c_int), ("reserved", c_int),
-        ("row_pos", c_void_p), ("row_kv", c_void_p),
+        ("row_pos", c_void_p), ("row_kv", c_void_p), ("gz", c_void_p),
     ]
 
 

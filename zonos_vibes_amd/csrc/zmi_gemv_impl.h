@@ -30,7 +30,7 @@
 
 namespace zmi_gemv {
 
-constexpr int PRO_PLAIN = 0, PRO_LN = 1;
+constexpr int PRO_PLAIN = 0, PRO_LN = 1, PRO_ADDLN = 2, PRO_GRMS = 3;
 constexpr size_t LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
 // DPP row_ror:8 — lane i of each 16-lane row reads lane (i + 8) & 15 of the same row
@@ -53,14 +53,45 @@ __device__ __forceinline__ void dma_piece(const bf16_t* gsrc, bf16_t* ldp) {
 }
 
 // LDS image: rows of x at a stride of K + 8 bf16 (2K + 16 bytes: the 16 rows of an MFMA
-// A-fragment read fall on distinct 16-byte bank slots), gamma / beta, then the segment sums.
+// A-fragment read fall on distinct 16-byte bank slots), the aux rows (ADDLN residual / GRMS z) at the
+// same stride, gamma (/ beta), then the segment sums.
 template <int K>
 struct Img {
   static constexpr int XROW = K + 8;
-  static size_t bytes(int rows, int nwv, int rt, bool ln) {
-    return (size_t)rows * XROW * 2 + (ln ? (size_t)4 * K : 0) + (size_t)nwv * 8 * rt * 4;
+  static constexpr int GROW = K + 8;  // f32 gate rows (GRMS)
+  static size_t bytes(int rows, int nwv, int rt, int pro) {
+    const size_t gb = (pro == PRO_LN || pro == PRO_ADDLN) ? (size_t)4 * K : (pro == PRO_GRMS ? (size_t)2 * K : 0);
+    const size_t aux = pro == PRO_ADDLN ? (size_t)rows * XROW * 2 : (pro == PRO_GRMS ? (size_t)rows * GROW * 4 : 0);
+    return (size_t)rows * XROW * 2 + aux + gb + (size_t)nwv * 8 * rt * 4;
   }
 };
+
+// fp32 sum of one 8-element chunk of x + aux (ADDLN: layer_norm_fn's fp32 residual sum), or of its
+// squared deviations; pairs added as (a + b), the order of ln_chunk_sum and zmi_add_layernorm
+__device__ __forceinline__ float addln_chunk_sum(const uint4& hv, const uint4& rv, float mean, bool sq) {
+  const uint32_t h[4] = {hv.x, hv.y, hv.z, hv.w}, r[4] = {rv.x, rv.y, rv.z, rv.w};
+  float t = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s0 = bf2f(h[j]) + bf2f(r[j]), s1 = bf2f(h[j] >> 16) + bf2f(r[j] >> 16);
+    if (sq) {
+      const float d0 = s0 - mean, d1 = s1 - mean;
+      t += d0 * d0 + d1 * d1;
+    } else {
+      t += s0 + s1;
+    }
+  }
+  return t;
+}
+// RMSNormGated's g = y * gate of element e of a chunk (fp32; gate = z * sigmoid(z), zmi_mamba2_step), the
+// value zmi_gated_rmsnorm forms as y * (z * sigmoid(z))
+__device__ __forceinline__ float gate_elem(const uint32_t (&y)[4], const float (&gz)[8], int e) {
+  return bf2f(y[e >> 1] >> (16 * (e & 1))) * gz[e];
+}
+__device__ __forceinline__ void load_gate(const float* p, float (&gz)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  gz[0] = a.x; gz[1] = a.y; gz[2] = a.z; gz[3] = a.w; gz[4] = b.x; gz[5] = b.y; gz[6] = b.z; gz[7] = b.w;
+}
 
 // Diagnostic build only (-DZMI_GEMV_STAMPS, tools/gemv_stamps.py): thread 0 of every workgroup
 // writes s_memrealtime (100 MHz) at phase boundaries into diag[reserved][block][8].
@@ -108,10 +139,15 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   const int alloc_rows = a.M < RT ? a.M : RT;
   const int row0 = rt * RT;
   const int rows = min(RT, a.M - row0);
+  constexpr bool AUX = PRO == PRO_ADDLN || PRO == PRO_GRMS;
+  constexpr int GB = (PRO == PRO_LN || PRO == PRO_ADDLN) ? 2 : (PRO == PRO_GRMS ? 1 : 0);  // gamma / beta rows
+  constexpr int GROW = Img<K>::GROW;
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* gam = xs + (size_t)alloc_rows * XROW;
+  bf16_t* xa = xs + (size_t)alloc_rows * XROW;  // aux rows: ADDLN bf16 residual, GRMS f32 gate
+  float* xg = reinterpret_cast<float*>(xa);
+  bf16_t* gam = xa + (PRO == PRO_ADDLN ? (size_t)alloc_rows * XROW : (PRO == PRO_GRMS ? (size_t)alloc_rows * GROW * 2 : 0));
   bf16_t* bet = gam + K;
-  float* red = reinterpret_cast<float*>(smem + (size_t)alloc_rows * XROW * 2 + (PRO == PRO_LN ? 4 * K : 0));
+  float* red = reinterpret_cast<float*>(gam + (size_t)GB * K);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SGPR descriptors, no waterfalls
@@ -127,13 +163,24 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   {
     constexpr int PPR = K / 512;
     const int n_x = rows * PPR;
-    const int n_pc = n_x + (PRO == PRO_LN ? 2 * PPR : 0);
+    constexpr int APR = PRO == PRO_GRMS ? 2 * PPR : PPR;  // aux pieces per row (f32 gate rows: twice the bytes)
+    const int n_a = AUX ? rows * APR : 0;
+    const int n_pc = n_x + n_a + GB * PPR;
+    const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)row0 * a.ld_aux * (PRO == PRO_GRMS ? 2 : 1)
+                           : nullptr;
     for (int pc = wave; pc < n_pc; pc += NWV) {
       if (pc < n_x) {
         const int r = pc / PPR, p = pc - r * PPR;
         dma_piece(X + (size_t)r * a.ldx + p * 512 + lane * 8, xs + r * XROW + p * 512);
+      } else if (pc < n_x + n_a) {
+        const int r = (pc - n_x) / APR, p = (pc - n_x) - r * APR;
+        if (PRO == PRO_GRMS)  // 1 KiB = 256 f32 of the gate row
+          dma_piece(XA + ((size_t)r * a.ld_aux + p * 256) * 2 + lane * 8,
+                    reinterpret_cast<bf16_t*>(xg + r * GROW + p * 256));
+        else
+          dma_piece(XA + (size_t)r * a.ld_aux + p * 512 + lane * 8, xa + r * XROW + p * 512);
       } else {
-        const int q = pc - n_x, which = q / PPR, p = q - which * PPR;
+        const int q = pc - n_x - n_a, which = q / PPR, p = q - which * PPR;
         const bf16_t* src = reinterpret_cast<const bf16_t*>(which ? a.ln_b : a.ln_w);
         dma_piece(src + p * 512 + lane * 8, (which ? bet : gam) + p * 512);
       }
@@ -216,6 +263,118 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
         const uint4 xv = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
         *reinterpret_cast<uint4*>(xr + (lane + 64 * i) * 8) = ln_apply(
             xv, *reinterpret_cast<const uint4*>(gam + c * 8), *reinterpret_cast<const uint4*>(bet + c * 8), rstd, nbias);
+      }
+    }
+    __syncthreads();
+  }
+  if (PRO == PRO_ADDLN) {
+    // layer_norm_fn prenorm: s = x + residual (fp32), LayerNorm(s) with (s - mean) rstd w + b; the column
+    // block 0 workgroup of each row tile writes bf16(s), the next block's residual
+    constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
+    float* part = red;
+    const int ntask = rows * NQ;
+    auto pass = [&](int task, float mean, bool sq) {
+      const int r = task / NQ, q = task - r * NQ;
+      const bf16_t* hr = xs + r * XROW + q * (K / NQ);
+      const bf16_t* rr = xa + r * XROW + q * (K / NQ);
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i)
+        t += addln_chunk_sum(*reinterpret_cast<const uint4*>(hr + (lane + 64 * i) * 8),
+                             *reinterpret_cast<const uint4*>(rr + (lane + 64 * i) * 8), mean, sq);
+      return wave_sum(t);
+    };
+    for (int task = wave; task < ntask; task += NWV) {
+      const float v = pass(task, 0.f, false);
+      if (lane == 0) part[task] = v;
+    }
+    __syncthreads();
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ;
+      const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
+      const float v = pass(task, mean, true);
+      if (lane == 0) part[RT * NQ + task] = v;
+    }
+    __syncthreads();
+    const bool wres = a.res_out != nullptr && cb == 0;
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ, q = task - r * NQ;
+      const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
+      const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part + RT * NQ + r * NQ) / (float)K + a.eps);
+      bf16_t* hr = xs + r * XROW + q * (K / NQ);
+      const bf16_t* rr = xa + r * XROW + q * (K / NQ);
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i) {
+        const int c = q * (K / NQ) / 8 + lane + 64 * i;
+        const uint4 hv = *reinterpret_cast<const uint4*>(hr + (lane + 64 * i) * 8);
+        const uint4 rv = *reinterpret_cast<const uint4*>(rr + (lane + 64 * i) * 8);
+        const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8), gbv = *reinterpret_cast<const uint4*>(bet + c * 8);
+        const uint32_t h[4] = {hv.x, hv.y, hv.z, hv.w}, rs[4] = {rv.x, rv.y, rv.z, rv.w};
+        const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w}, ub[4] = {gbv.x, gbv.y, gbv.z, gbv.w};
+        uint32_t o[4], so[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float s0 = bf2f(h[j]) + bf2f(rs[j]), s1 = bf2f(h[j] >> 16) + bf2f(rs[j] >> 16);
+          const float y0 = ((s0 - mean) * rstd) * bf2f(uw[j]) + bf2f(ub[j]);
+          const float y1 = ((s1 - mean) * rstd) * bf2f(uw[j] >> 16) + bf2f(ub[j] >> 16);
+          o[j] = f2bf(y0) | (f2bf(y1) << 16);
+          so[j] = f2bf(s0) | (f2bf(s1) << 16);
+        }
+        *reinterpret_cast<uint4*>(hr + (lane + 64 * i) * 8) = uint4{o[0], o[1], o[2], o[3]};
+        if (wres)
+          reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.res_out) + (size_t)(row0 + r) * a.ld_aux)[c] =
+              uint4{so[0], so[1], so[2], so[3]};
+      }
+    }
+    __syncthreads();
+  }
+  if (PRO == PRO_GRMS) {
+    // RMSNormGated (norm_before_gate=False): g = y (z sigmoid(z)), out = g rstd w; g recomputed in the
+    // apply pass (the same bits), sums of g^2 element by element as zmi_gated_rmsnorm
+    constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
+    float* part = red;
+    const int ntask = rows * NQ;
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ, q = task - r * NQ;
+      const bf16_t* yr = xs + r * XROW + q * (K / NQ);
+      const float* zr = xg + r * GROW + q * (K / NQ);
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i) {
+        const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+        const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
+        float gz[8];
+        load_gate(zr + (lane + 64 * i) * 8, gz);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = gate_elem(y, gz, e);
+          t += g * g;
+        }
+      }
+      t = wave_sum(t);
+      if (lane == 0) part[task] = t;
+    }
+    __syncthreads();
+    for (int task = wave; task < ntask; task += NWV) {
+      const int r = task / NQ, q = task - r * NQ;
+      const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part + r * NQ) / (float)K + a.eps);
+      bf16_t* yr = xs + r * XROW + q * (K / NQ);
+      const float* zr = xg + r * GROW + q * (K / NQ);
+#pragma unroll
+      for (int i = 0; i < CPQ; ++i) {
+        const int c = q * (K / NQ) / 8 + lane + 64 * i;
+        const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+        const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
+        const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
+        const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
+        float gz[8];
+        load_gate(zr + (lane + 64 * i) * 8, gz);
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = f2bf((gate_elem(y, gz, 2 * j) * rstd) * bf2f(uw[j])) |
+                 (f2bf((gate_elem(y, gz, 2 * j + 1) * rstd) * bf2f(uw[j] >> 16)) << 16);
+        *reinterpret_cast<uint4*>(yr + (lane + 64 * i) * 8) = uint4{o[0], o[1], o[2], o[3]};
       }
     }
     __syncthreads();
@@ -371,7 +530,7 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
   auto fn = gemv_kernel<G, W, NL, RT, PRO, EPI, NTW>;
   const int n_cb = (a.N / 8 + G - 1) / G;
   const int n_rt = (a.M + RT - 1) / RT;
-  const size_t lds = Img<K>::bytes(a.M < RT ? a.M : RT, G * W, RT, PRO == PRO_LN);
+  const size_t lds = Img<K>::bytes(a.M < RT ? a.M : RT, G * W, RT, PRO);
   if (lds > LDS_MAX) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
     static const hipError_t attr =  // once per instantiation: allow > 64 KiB of dynamic LDS
@@ -387,8 +546,19 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
 
 template <int G, int W, int NL, int RT, int EPI>
 hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
+  constexpr int K = W * NL * 64;
   const bool ln = a.ln_w != nullptr;
   const bool once = a.M <= RT;  // each weight read once: non-temporal loads
+  if (a.pro == ZMI_PRO_ADDLN) {  // the hybrid blocks' d_model GEMVs
+    if constexpr ((K == 512 || K == 2048) && EPI != ZMI_EPI_RESIDUAL && EPI != ZMI_EPI_F32)
+      return once ? launch_p<G, W, NL, RT, PRO_ADDLN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_ADDLN, EPI, 0>(a, s);
+    return hipErrorInvalidValue;
+  }
+  if (a.pro == ZMI_PRO_GRMS) {  // the Mamba2 out_proj (K = d_ssm)
+    if constexpr ((K == 1024 || K == 4096) && EPI == ZMI_EPI_STORE)
+      return once ? launch_p<G, W, NL, RT, PRO_GRMS, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_GRMS, EPI, 0>(a, s);
+    return hipErrorInvalidValue;
+  }
   if (ln) return once ? launch_p<G, W, NL, RT, PRO_LN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_LN, EPI, 0>(a, s);
   return once ? launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 0>(a, s);
 }

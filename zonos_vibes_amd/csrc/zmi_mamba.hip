@@ -114,8 +114,13 @@ __global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args 
 #pragma unroll
   for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = sv[j];
   out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
-  if (nq == 0)
+  if (nq == 0) {
     reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * a.D[h]);
+    if (a.gz) {  // RMSNormGated's gate of this channel, once (the out_proj GEMV's GRMS prologue multiplies)
+      const float zz = bf2f(zx[h * MB_HD + p]);
+      a.gz[(size_t)m * a.ldy + h * MB_HD + p] = zz * (1.0f / (1.0f + expf(-zz)));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------- prefill scan
@@ -254,13 +259,13 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const bf16_t* hid, int ldh,
     }
   }
   const float mean = block_sum4(sum, part) / (float)K;
-  float sq = 0.f;
+  float sq = 0.f;  // pairs as (a + b): the GEMV ADDLN prologue's order (zmi_gemv_impl.h addln_chunk_sum)
 #pragma unroll
   for (int i = 0; i < CPL; ++i)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = v[i][e] - mean;
-      sq += on ? d * d : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const float d0 = v[i][2 * e] - mean, d1 = v[i][2 * e + 1] - mean;
+      sq += on ? d0 * d0 + d1 * d1 : 0.f;
     }
   const float rstd = 1.0f / sqrtf(block_sum4(sq, part) / (float)K + eps);
   if (!on) return;

@@ -5,13 +5,15 @@ mamba-ssm 2.2.4's create_block (absent here: parity unpinned, oracle/hybrid_cpu.
 around the backbone — delay pattern, prefill orchestration, heads, CFG, sampler, EOS state machine,
 hipGraph-captured decode loop, slots — is HipEngine's; this class only swaps the layer plan:
 
-  every block    zmi_add_layernorm (layer_norm_fn prenorm: residual += hidden in fp32, LayerNorm)
+  every block    layer_norm_fn prenorm (residual += hidden in fp32, LayerNorm): decode as the ADDLN
+                 prologue of the block's first GEMV, prefill as zmi_add_layernorm (same arithmetic)
   Mamba2 block   in_proj GEMV -> zmi_mamba2_step (conv ring + SiLU + selective state update)
-                 -> zmi_gated_rmsnorm -> out_proj GEMV      (prefill: zmi_mamba2_scan over the sequence)
+                 -> out_proj GEMV with the GRMS prologue (RMSNormGated; prefill: zmi_gated_rmsnorm and
+                 zmi_mamba2_scan over the sequence)
   MHA block      QKV GEMV (non-interleaved rotary as interleaved pairs on permuted q / k rows, bf16
                  cos / sin as flash-attn caches them) -> attention kernel -> out_proj GEMV
-  optional MLP   zmi_add_layernorm -> fc1 SwiGLU GEMV -> fc2 GEMV       (d_intermediate > 0)
-  norm_f         zmi_add_layernorm (hidden + residual) -> heads GEMV
+  optional MLP   (add + LayerNorm) fc1 SwiGLU GEMV -> fc2 GEMV       (d_intermediate > 0)
+  norm_f         (add + LayerNorm) heads GEMV
 
 State per slot row: the conv ring bf16 [4][conv_dim] and the SSM state bf16 [nheads][64][128] of
 every Mamba2 layer (1.06 MB per row and layer at the Zonos-v0.1-hybrid dims), K / V of the attention
@@ -70,7 +72,10 @@ class HybridEngine(HipEngine):
         z = lambda *shape, dt=torch.bfloat16: torch.zeros(*shape, dtype=dt, device=dev)  # noqa: E731
         with torch.cuda.stream(self.stream):
             self.hid, self.nrm = z(R, self.d), z(R, self.d)
+            self.x2 = z(R, self.d)  # the decode residual stream ping-pongs between self.x and self.x2
+            self.zero_rows = z(R, self.d)  # block 0's "hidden": s = 0 + residual, exactly the residual
             self.zx, self.yb, self.yn = z(R, md["d_in_proj"]), z(R, md["d_ssm"]), z(R, md["d_ssm"])
+            self.gz = z(R, md["d_ssm"], dt=torch.float32)  # RMSNormGated's gate z * sigmoid(z) (decode)
             self.hid_pre, self.nrm_pre = z(2 * P, self.d), z(2 * P, self.d)
             self.zx_pre, self.yb_pre, self.yn_pre = z(2 * P, md["d_in_proj"]), z(2 * P, md["d_ssm"]), z(2 * P, md["d_ssm"])
             self.hm = z(R, max(self.Fm, self.F, 1))
@@ -208,16 +213,70 @@ class HybridEngine(HipEngine):
         return items
 
     # ------------------------------------------------------------------ decode plan
+    def _fused(self, item, pro, aux, ld_aux, res_out=None):
+        a, epi = item
+        a.pro, a.aux, a.ld_aux, a.res_out = pro, aux.data_ptr(), ld_aux, _lib.ptr(res_out)
+        return ("gemv", (a, epi))
+
     def _plan(self, rows: int) -> list:
+        """Decode launches. The block norms run as GEMV prologues: layer_norm_fn(hidden, residual) as ADDLN
+        on the consuming GEMV (in_proj / qkv / fc1 / heads; the new residual goes to the other of two
+        buffers, since the other workgroups still read the old one), RMSNormGated as GRMS on out_proj (up
+        to 4 rows, the gate z * sigmoid(z) formed once per channel by the Mamba2 step kernel: the y and f32
+        gate rows of a larger tile would not fit the LDS image). Same arithmetic as the
+        prefill's standalone norm kernels."""
         if rows not in self._plans:
-            w = self.w
+            w, d, md, qd = self.w, self.d, self.md, self.H * self.hd
+            res = [self.x, self.x2]
+            cur = 0
             plan = []
+
+            def normed_gemv(item, ln, first):
+                nonlocal cur
+                item[0].ln_w, item[0].ln_b = ln[0].data_ptr(), ln[1].data_ptr()
+                if first:  # block 0 (residual=None): hidden = 0, so s is the embedding and stays the residual
+                    return self._fused(item, _lib.PRO_ADDLN, res[cur], d, None)
+                out = self._fused(item, _lib.PRO_ADDLN, res[cur], d, res[1 - cur])
+                cur = 1 - cur
+                return out
+
             for i, lw in enumerate(w["layers"]):
-                plan += self._layer_items(lw, rows, self.x, self.hid, self.nrm, self.zx, self.yb, self.yn, self.hm,
-                                          self.q, self.attn, self.row_kv, self.row_pos, first=(i == 0))
-            plan.append(("call", self._addln(self.hid, self.x, (w["nf_w"], w["nf_b"]), self.nrm, rows, store=False)))
-            plan.append(("gemv", self._gemv(w["heads"], self.nrm, rows, HEADS_N_PAD, self.d, _lib.EPI_LOGITS,
-                                            self.logits, 0, n_valid=HEADS_N)))
+                x_in = self.zero_rows if i == 0 else self.hid
+                ln1 = (lw["ln1_w"], lw["ln1_b"])
+                if lw["kind"] == "attn":
+                    j = lw["kv"]
+                    qkv_n = (self.H + 2 * self.Hkv) * self.hd
+                    plan.append(normed_gemv(self._gemv(lw["qkv"], x_in, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                                       kv=(self.kc[j], self.vc[j]), row_kv=self.row_kv,
+                                                       row_pos=self.row_pos), ln1, i == 0))
+                    plan.append(("attn", j))
+                    plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)))
+                else:
+                    plan.append(normed_gemv(self._gemv(lw["in_proj"], x_in, rows, md["d_in_proj"], d, _lib.EPI_STORE,
+                                                       self.zx, md["d_in_proj"]), ln1, i == 0))
+                    sa = self._mamba_args(lw, self.zx, self.yb, rows, self.row_pos, None)
+                    fuse_g = rows <= 4  # the f32 gate rows of a larger tile would not fit the LDS image
+                    if fuse_g:
+                        sa.gz = self.gz.data_ptr()
+                    plan.append(("call", self._call_step(sa)))
+                    out = self._gemv(lw["out"], self.yb, rows, d, md["d_ssm"], _lib.EPI_STORE, self.hid, d)
+                    if fuse_g:
+                        out[0].ln_w = lw["norm_w"].data_ptr()
+                        out[0].eps = 1e-5  # RMSNormGated's own eps (mamba2.py)
+                        plan.append(self._fused(out, _lib.PRO_GRMS, self.gz, md["d_ssm"]))
+                    else:
+                        plan.append(("call", self._gnorm(lw, self.yb, self.zx, self.yn, rows)))
+                        plan.append(("gemv", self._gemv(lw["out"], self.yn, rows, d, md["d_ssm"], _lib.EPI_STORE,
+                                                        self.hid, d)))
+                if lw.get("ff"):
+                    ff = lw["ff"]
+                    plan.append(normed_gemv(self._gemv(lw["fc1"], self.hid, rows, 2 * ff, d, _lib.EPI_SWIGLU, self.hm,
+                                                       ff), (lw["ln2_w"], lw["ln2_b"]), False))
+                    plan.append(("gemv", self._gemv(lw["fc2"], self.hm, rows, d, ff, _lib.EPI_STORE, self.hid, d)))
+            heads = self._gemv(w["heads"], self.hid, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
+                               n_valid=HEADS_N)
+            heads[0].ln_w, heads[0].ln_b = w["nf_w"].data_ptr(), w["nf_b"].data_ptr()
+            plan.append(self._fused(heads, _lib.PRO_ADDLN, res[cur], d, None))
             self._plans[rows] = plan
         return self._plans[rows]
 
