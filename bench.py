@@ -265,6 +265,38 @@ def time_hybrid(dev, n_new: int) -> dict:
     return out
 
 
+def time_batch(model, dev, n_utt: int = 64, slots: int = 64) -> dict:
+    """A bounded C3-shaped sample on one GPU: n_utt independent utterances of 2-6 s (Lc = 8 + 15 s, as
+    SURVEY.md §8d C3 draws them, shorter so the run stays short) through `slots` continuous-batching
+    slots (generate_batch: LPT order, slot refill at chunk boundaries), greedy, EOS suppressed, + DAC
+    decode of every utterance. Aggregate real-time factor = total audio s / wall s. Runs last: it grows
+    the engine to `slots` slots."""
+    g = torch.Generator().manual_seed(7)
+    secs = (2.0 + 4.0 * torch.rand(n_utt, generator=g)).tolist()
+    d = model.config.backbone.d_model
+    conds = [cond_tensor(100 + i, d, dev)[:, : 8 + round(15 * s)].contiguous() for i, s in enumerate(secs)]
+    n_new = [max(1, round(s * DAC_SAMPLE_RATE / DAC_HOP)) for s in secs]
+    sp = dict(temperature=0.0)
+    model.generate_batch(conds[:2], max_new_tokens=[16, 16], sampling_params=sp, seeds=[0, 1], max_slots=slots)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = model.generate_batch(conds, max_new_tokens=n_new, sampling_params=sp, seeds=list(range(n_utt)),
+                               max_slots=slots)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for c in out:
+        model.autoencoder.decode(c)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    frames = sum(int(c.shape[-1]) for c in out)
+    assert frames == sum(n_new)
+    audio = frames * DAC_HOP / DAC_SAMPLE_RATE
+    return {"config": f"C3 sample: {n_utt} utterances of 2-6 s (Lc 8 + 15 s), {slots} slots on one GPU, greedy, "
+                      f"EOS suppressed, + DAC decode per utterance",
+            "rtf": round(audio / (t2 - t0), 2), "audio_s": round(audio, 1), "generate_s": round(t1 - t0, 3),
+            "dac_s": round(t2 - t1, 3), "frames_per_s": round(frames / (t2 - t0), 1)}
+
+
 def cpu_cores() -> int:
     """CPU threads available to this process: its affinity set, capped by OMP_NUM_THREADS when the host
     sets one (the GPU box gives each GPU a 16-thread share and sets OMP_NUM_THREADS=16)."""
@@ -332,6 +364,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--new-tokens", type=int, default=N_NEW)
     ap.add_argument("--no-hybrid", action="store_true", help="skip the C4 hybrid-backbone line in `widened`")
+    ap.add_argument("--no-batch", action="store_true", help="skip the C3-sample batch line in `widened`")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -405,6 +438,8 @@ def main():
     if rank == 0 and not args.no_hybrid:
         widened["hybrid_c4"] = time_hybrid(dev, n_new)
     breakdown = utterance_breakdown(model, cond, n_new)
+    if rank == 0 and not args.no_batch:
+        widened["batch_c3_sample"] = time_batch(model, dev)  # last: grows the engine to 64 slots
     out = None
     if rank == 0:
         achieved = bl / (us * 1e-6) / 1e9

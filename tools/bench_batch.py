@@ -1,0 +1,25 @@
+"""The bench's C3-shaped batch sample (64 mixed-length utterances through 64 slots) under a profiler.
+
+    rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o bprof -- python tools/bench_batch.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from zonos_vibes_amd.config import zonos_v01_transformer  # noqa: E402
+from zonos_vibes_amd.model import Zonos  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=bench.LC + bench.N_NEW + 9,
+                        max_prefill=bench.LC + 1)
+    print(json.dumps(bench.time_batch(m, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,7 @@
 //    two-pass statistics, bf16-rounded output, the same arithmetic for every row.
 //  * fused epilogues: bf16 store, residual add, RoPE + KV-cache write, SwiGLU, logits, raw f32.
 #pragma once
+#include <algorithm>
 #include "zmi_common.h"
 #include "zmi_kernels.h"
 
@@ -123,7 +124,7 @@ struct QkvFuse {
 
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW, int FUSE = 0>
 __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_rt, int b, char* smem,
-                                          const QkvFuse& fz) {
+                                          const QkvFuse& fz, int rpw = 1) {
   constexpr int K = W * NL * 64;
   constexpr int KC = K / 64;
   constexpr int NWV = G * W;
@@ -131,14 +132,19 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   static_assert(RT == 8 || RT == 16, "row tile");
   static_assert(!FUSE || EPI == ZMI_EPI_QKV, "only the QKV projection hands off in-launch");
 
-  // block -> (column block, row tile): the row tiles of one column block take ids 8 apart
+  // block -> (column block, group of rpw row tiles): the groups of one column block take ids 8 apart.
+  // A workgroup keeps its weight slice in registers and runs its row tiles one after the other, each
+  // with the arithmetic of a lone tile (a row's result does not depend on rpw or M).
   const int idx = b >> 3;
-  const int cb = (idx / n_rt) * 8 + (b & 7), rt = idx - (idx / n_rt) * n_rt;
+  const int n_rg = (n_rt + rpw - 1) / rpw;
+  const int cb = (idx / n_rg) * 8 + (b & 7), rg = idx - (idx / n_rg) * n_rg;
   if (cb >= n_cb) return;  // padding block: exits before any barrier
   ZMI_GSTAMP(0);
   const int alloc_rows = a.M < RT ? a.M : RT;
-  const int row0 = rt * RT;
-  const int rows = min(RT, a.M - row0);
+  int rt = rg * rpw;
+  const int rt_end = min(n_rt, rt + rpw);
+  int row0 = rt * RT;
+  int rows = min(RT, a.M - row0);
   constexpr bool AUX = PRO == PRO_ADDLN || PRO == PRO_GRMS;
   constexpr int GB = (PRO == PRO_LN || PRO == PRO_ADDLN) ? 2 : (PRO == PRO_GRMS ? 1 : 0);  // gamma / beta rows
   constexpr int GROW = Img<K>::GROW;
@@ -158,14 +164,21 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   const int g = g_ok ? g_raw : ngroups - 1;  // clamped: every wave joins the barriers
   const int col0 = g * 8;
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)row0 * a.ldx;
+  // epilogue operands that need no other load (older than the weights: covered by the vmcnt below).
+  // The group's first wave runs the epilogue; its lane handles outputs e = lane + 64 i.
+  const bool ew = (wk == 0) && g_ok;
+  constexpr int NE = (8 * RT + 63) / 64;
+  uint32_t res_pre[NE];
+  int q_pos = -1, q_kvr = 0;
 
-  // (1) activation rows (+ LayerNorm gamma / beta) into LDS by DMA, 1 KiB pieces spread over waves
-  {
+  // (1) activation rows (+ LayerNorm gamma / beta, first tile only) into LDS by DMA, 1 KiB pieces
+  // spread over waves; then the tile's epilogue operands
+  auto stage = [&](bool first) {
     constexpr int PPR = K / 512;
     const int n_x = rows * PPR;
     constexpr int APR = PRO == PRO_GRMS ? 2 * PPR : PPR;  // aux pieces per row (f32 gate rows: twice the bytes)
     const int n_a = AUX ? rows * APR : 0;
-    const int n_pc = n_x + n_a + GB * PPR;
+    const int n_pc = n_x + n_a + (first ? GB * PPR : 0);
     const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)row0 * a.ld_aux * (PRO == PRO_GRMS ? 2 : 1)
                            : nullptr;
     for (int pc = wave; pc < n_pc; pc += NWV) {
@@ -185,27 +198,24 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
         dma_piece(src + p * 512 + lane * 8, (which ? bet : gam) + p * 512);
       }
     }
-  }
-  // epilogue operands that need no other load (older than the weights: covered by the vmcnt below).
-  // The group's first wave runs the epilogue; its lane handles outputs e = lane + 64 i.
-  const bool ew = (wk == 0) && g_ok;
-  constexpr int NE = (8 * RT + 63) / 64;
-  uint32_t res_pre[NE];
 #pragma unroll
-  for (int i = 0; i < NE; ++i) res_pre[i] = 0;
-  int q_pos = -1, q_kvr = 0;
-  if (EPI == ZMI_EPI_RESIDUAL && ew) {
+    for (int i = 0; i < NE; ++i) res_pre[i] = 0;
+    q_pos = -1;
+    q_kvr = 0;
+    if (EPI == ZMI_EPI_RESIDUAL && ew) {
 #pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int e = lane + 64 * i, r = e >> 3, n = col0 + (e & 7);
-      if (r < rows && n < a.n_valid)
-        res_pre[i] = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + n];
+      for (int i = 0; i < NE; ++i) {
+        const int e = lane + 64 * i, r = e >> 3, n = col0 + (e & 7);
+        if (r < rows && n < a.n_valid)
+          res_pre[i] = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + n];
+      }
     }
-  }
-  if (EPI == ZMI_EPI_QKV && ew && (lane >> 2) < rows) {
-    q_pos = a.row_pos[row0 + (lane >> 2)];
-    q_kvr = a.row_kv[row0 + (lane >> 2)];
-  }
+    if (EPI == ZMI_EPI_QKV && ew && (lane >> 2) < rows) {
+      q_pos = a.row_pos[row0 + (lane >> 2)];
+      q_kvr = a.row_kv[row0 + (lane >> 2)];
+    }
+  };
+  stage(true);
   __builtin_amdgcn_sched_barrier(0);
   // (2) the whole weight slice of this lane, in flight at once: one buffer descriptor per wave
   // (wave-uniform base), lane offset in the VGPR, chunk offset j KiB folded into the instruction
@@ -219,6 +229,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   __builtin_amdgcn_sched_barrier(0);
   ZMI_GSTAMP(1);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // DMA pieces + epilogue operands landed
+  for (;;) {  // the workgroup's row tiles
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   ZMI_GSTAMP(2);
@@ -409,7 +420,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   }
   __syncthreads();
   ZMI_GSTAMP(5);
-  if (!ew) return;
+  if (ew) {
   auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
     float v = red[((gi * W) * 8 + c) * RT + r];
 #pragma unroll
@@ -489,13 +500,31 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
                 (uint64_t)packed | ((uint64_t)(unsigned)(q_pos + 1) << 32));
     }
   }
+  }  // ew
   ZMI_GSTAMP(6);
+  // one tile when each weight is read once (NTW: M <= RT, every decode launch): no loop state there
+  if (NTW || ++rt >= rt_end) break;
+  __syncthreads();  // every wave is done with this tile's LDS image and segment sums
+  row0 = rt * RT;
+  rows = min(RT, a.M - row0);
+  X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)row0 * a.ldx;
+  stage(false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's rows (the weights landed long ago)
+  }  // row tiles
 }
 
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
-__global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt) {
+__global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt, int rpw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  gemv_body<G, W, NL, RT, PRO, EPI, NTW>(a, n_cb, n_rt, blockIdx.x, smem, QkvFuse{nullptr, 0});
+  gemv_body<G, W, NL, RT, PRO, EPI, NTW>(a, n_cb, n_rt, blockIdx.x, smem, QkvFuse{nullptr, 0}, rpw);
+}
+
+// row tiles per workgroup: enough workgroups to fill the chip (~4 per CU), each re-reading its weight
+// slice as few times as that allows (speed only: a row's arithmetic does not depend on it)
+inline int rows_per_wg(int n_cb, int n_rt) {
+  if (n_rt <= 1) return 1;
+  const int n_rg = std::max(1, std::min(n_rt, 1024 / std::max(1, n_cb)));
+  return (n_rt + n_rg - 1) / n_rg;
 }
 
 // (W, NL, RT) from K: K = 64 W NL. The shape fixes a row's reduction order, so it depends on K
@@ -538,9 +567,10 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
                             (int)LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
-  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * n_rt;
+  const int rpw = rows_per_wg(n_cb, n_rt);
+  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * ((n_rt + rpw - 1) / rpw);
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt, rpw);
   return hipGetLastError();
 }
 

@@ -120,6 +120,7 @@ class HipEngine:
         z = lambda *shape, dt=torch.bfloat16: torch.zeros(*shape, dtype=dt, device=dev)  # noqa: E731
         with torch.cuda.stream(self.stream):
             self.x, self.q, self.attn = z(R, d), z(R, qd), z(R, qd)
+            self.xn = z(R, d)  # LayerNorm'd rows of a many-slot decode step (pre-pass, > 16 rows)
             self.h = z(R, self.F)
             self.logits = z(R, N_CODEBOOKS, 1026, dt=torch.float32)
             self.row_kv = z(R, dt=torch.int32)
@@ -253,11 +254,25 @@ class HipEngine:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
             fused = self._use_attn_block(rows)
+            # above one 16-row tile every column-block workgroup would LayerNorm every row: normalise once
+            # per layer instead (zmi_layernorm_rows, the prologue's bits) and run the GEMVs on plain rows
+            pre = rows > 16
             plan = []
+
+            def normed(ln):
+                """(activation rows, prologue LayerNorm) of a LayerNorm'd GEMV, with the pre-pass item."""
+                if not pre:
+                    return self.x, ln
+                plan.append(("call", lambda ln=ln: _lib.check(self.lib.zmi_layernorm_rows(
+                    self.x.data_ptr(), d, rows, d, ln[0].data_ptr(), ln[1].data_ptr(), self.eps, self.xn.data_ptr(),
+                    d, self.sptr), "ln")))
+                return self.xn, None
+
             for i, lw in enumerate(w["layers"]):
                 kv = (self.kc[i], self.vc[i])
-                qkv = self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                 ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
+                xin, ln = normed((lw["ln1_w"], lw["ln1_b"])) if not fused else (self.x, (lw["ln1_w"], lw["ln1_b"]))
+                qkv = self._gemv(lw["qkv"], xin, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                 ln=ln, kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
                 if fused:
                     pf = _lib.Prefetch()
                     if self.prefetch_blocks > 0:
@@ -270,11 +285,13 @@ class HipEngine:
                     plan.append(("gemv", qkv))
                     plan.append(("attn", i))
                 plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
-                plan.append(("gemv", self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
-                                                self.F, ln=(lw["ln2_w"], lw["ln2_b"]))))
+                xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
+                plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
+                                                self.F, ln=ln)))
                 plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
-            plan.append(("gemv", self._gemv(w["heads"], self.x, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
-                                            n_valid=HEADS_N, ln=(w["nf_w"], w["nf_b"]))))
+            xin, ln = normed((w["nf_w"], w["nf_b"]))
+            plan.append(("gemv", self._gemv(w["heads"], xin, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
+                                            n_valid=HEADS_N, ln=ln)))
             self._plans[rows] = plan
         return self._plans[rows]
 
