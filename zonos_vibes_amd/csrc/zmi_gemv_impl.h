@@ -545,12 +545,14 @@ inline bool shape_for(int K, bool ln, Shape* s) {
   return false;
 }
 
-// column groups per block: 2 for the many-group LayerNorm'd projections (qkv, fc1, heads: the
+// column groups per block: 2 for the many-group K = 2048 projections with a prologue or many rows (qkv, fc1, heads: the
 // block's LayerNorm and activation staging are then shared by 16 columns); `groups` > 0 overrides.
 // Speed only: a group's arithmetic does not depend on G.
 inline int groups_for(const ZmiGemvArgs& a, const Shape& s) {
   if (a.groups > 0) return a.groups;
-  return (a.ln_w != nullptr && a.K == 2048 && a.N / 8 >= 384) ? 2 : 1;
+  // two groups also for plain rows when there are many of them: each workgroup's activation tiles
+  // then serve 16 columns (a 128-row fc1 re-read its rows from L2 per 8-column group: ~1 GB a launch)
+  return (a.K == 2048 && a.N / 8 >= 384 && (a.ln_w != nullptr || a.pro != ZMI_PRO_AUTO || a.M > 16)) ? 2 : 1;
 }
 
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
