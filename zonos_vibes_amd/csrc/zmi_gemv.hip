@@ -51,8 +51,8 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
     return zmi_fail_msg("gemv: K must be 512, 1024, 2048, 4096 or 8192");
   if (a.M < 1) return zmi_fail_msg("gemv: M must be >= 1");
   if (a.ldx % 8) return zmi_fail_msg("gemv: ldx must be a multiple of 8 (16-byte rows)");
-  if (a.groups < 0 || a.groups > 2 || (a.groups == 2 && a.K != 2048))
-    return zmi_fail_msg("gemv: groups must be 0 (library choice), 1, or 2 for K = 2048");
+  if (a.groups < 0 || a.groups > 2 || (a.groups == 2 && a.K != 2048 && a.K != 8192))
+    return zmi_fail_msg("gemv: groups must be 0 (library choice), 1, or 2 for K = 2048 / 8192");
   if (a.pro != ZMI_PRO_AUTO && a.pro != ZMI_PRO_ADDLN && a.pro != ZMI_PRO_GRMS) return zmi_fail_msg("gemv: unknown prologue");
   if (a.pro == ZMI_PRO_ADDLN && (!a.ln_w || !a.ln_b || !a.aux || a.ld_aux % 8 || a.res_out == a.aux))
     return zmi_fail_msg("gemv: ADDLN needs ln_w, ln_b, aux (ld_aux % 8 == 0) and res_out != aux");

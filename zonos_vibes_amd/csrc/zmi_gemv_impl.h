@@ -552,6 +552,7 @@ inline int groups_for(const ZmiGemvArgs& a, const Shape& s) {
   if (a.groups > 0) return a.groups;
   // two groups also for plain rows when there are many of them: each workgroup's activation tiles
   // then serve 16 columns (a 128-row fc1 re-read its rows from L2 per 8-column group: ~1 GB a launch)
+  if (a.K == 8192 && a.M > 16 && a.N / 8 >= 256) return 2;  // fc2 over many rows: 16 KB activation rows
   return (a.K == 2048 && a.N / 8 >= 384 && (a.ln_w != nullptr || a.pro != ZMI_PRO_AUTO || a.M > 16)) ? 2 : 1;
 }
 
@@ -608,6 +609,7 @@ hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
   ZMI_SHAPE(2, 4, 8, 16)
   ZMI_SHAPE(1, 4, 16, 16)
   ZMI_SHAPE(1, 8, 16, 8)
+  ZMI_SHAPE(2, 8, 16, 8)
 #undef ZMI_SHAPE
   return hipErrorInvalidValue;  // e.g. groups = 2 outside the LayerNorm'd K = 2048 shape
 }
