@@ -297,6 +297,43 @@ def time_batch(model, dev, n_utt: int = 64, slots: int = 64) -> dict:
             "dac_s": round(t2 - t1, 3), "frames_per_s": round(frames / (t2 - t0), 1)}
 
 
+def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430) -> dict:
+    """One GPU's share of BASELINE config C5 (voice clone, long form): `slots` utterances of n_new frames
+    (60 s) after a `prefix`-frame audio prompt (random codes), Lc = 160, greedy, EOS suppressed, through
+    `slots` slots (contexts grow to Lc + prefix + n_new ~ 5.8k positions), then DAC decode of every
+    utterance's prefix + new frames. A fresh engine sized for the job."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_slots=slots, max_seqlen=LC + prefix + n_new + 9,
+                        max_prefill=LC + prefix + 1)
+    g = torch.Generator().manual_seed(11)
+    conds = [cond_tensor(200 + i, cfg.backbone.d_model, dev) for i in range(slots)]
+    prefixes = [torch.randint(0, 1024, (1, 9, prefix), generator=g).to(dev) for _ in range(slots)]
+    sp = dict(temperature=0.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = m.generate_batch(conds, prefixes, max_new_tokens=n_new, sampling_params=sp, seeds=list(range(slots)),
+                           max_slots=slots)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for c in out:
+        m.autoencoder.decode(c)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    frames = sum(int(c.shape[-1]) for c in out)
+    assert frames == slots * (prefix + n_new)
+    new_audio = slots * n_new * DAC_HOP / DAC_SAMPLE_RATE
+    res = {"config": f"C5 share of one GPU: {slots} voice-clone utterances, {prefix}-frame audio prefix + {n_new} new "
+                     f"frames (60 s), Lc {LC}, {slots} slots, greedy, EOS suppressed, + DAC decode of "
+                     f"{slots} x {prefix + n_new} frames",
+           "rtf_new_audio": round(new_audio / (t2 - t0), 2), "generate_s": round(t1 - t0, 2),
+           "dac_s": round(t2 - t1, 3), "dac_frames_per_s": round(frames / (t2 - t1), 1),
+           "decode_steps": n_new + 8, "ms_per_step": round((t1 - t0) / (n_new + 8) * 1e3, 3)}
+    del m
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_cores() -> int:
     """CPU threads available to this process: its affinity set, capped by OMP_NUM_THREADS when the host
     sets one (the GPU box gives each GPU a 16-thread share and sets OMP_NUM_THREADS=16)."""
@@ -365,6 +402,7 @@ def main():
     ap.add_argument("--new-tokens", type=int, default=N_NEW)
     ap.add_argument("--no-hybrid", action="store_true", help="skip the C4 hybrid-backbone line in `widened`")
     ap.add_argument("--no-batch", action="store_true", help="skip the C3-sample batch line in `widened`")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (voice clone, 60 s, 8 slots) line in `widened`")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -437,6 +475,8 @@ def main():
     widened = time_widened_rows(model, dev)
     if rank == 0 and not args.no_hybrid:
         widened["hybrid_c4"] = time_hybrid(dev, n_new)
+    if rank == 0 and not args.no_c5:
+        widened["c5_share"] = time_c5(dev)
     breakdown = utterance_breakdown(model, cond, n_new)
     if rank == 0 and not args.no_batch:
         widened["batch_c3_sample"] = time_batch(model, dev)  # last: grows the engine to 64 slots

@@ -254,9 +254,10 @@ class HipEngine:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
             fused = self._use_attn_block(rows)
-            # above one 16-row tile every column-block workgroup would LayerNorm every row: normalise once
-            # per layer instead (zmi_layernorm_rows, the prologue's bits) and run the GEMVs on plain rows
-            pre = rows > 16
+            # past a few rows every column-block workgroup's LayerNorm of all of them costs more than the
+            # launch that normalises them once per layer (fc1 at 16 rows: 30.7 us with the prologue);
+            # zmi_layernorm_rows gives the prologue's bits, so the plan may switch at any row count
+            pre = rows > 4
             plan = []
 
             def normed(ln):
