@@ -271,6 +271,13 @@ int zmi_add_layernorm(const void* hidden, int ldh, void* residual, int ldr, int 
 /* RMSNormGated(norm_before_gate=False): out = rmsnorm(y * silu(z)) * w, bf16; k in {512 .. 4096}. */
 int zmi_gated_rmsnorm(const void* y, int ldy, const void* z, int ldz, int m, int k, const void* w, float eps,
                       void* out, int ldo, void* stream);
+/* Decode: the Mamba2 in_proj GEMV (ADDLN prologue, K = 2048) and zmi_mamba2_step in ONE launch: the step
+ * workgroups load their state / conv-ring / conv-weight operands under the in_proj's weight stream and take
+ * the in_proj output from {pair, tag = position + 1} granules (`gran`: zmi_mamba_block_gran_words(M,
+ * d_in_proj) words, zeroed when a row starts an utterance); 1 <= M <= 16; bit-identical to the two
+ * separate launches; *err becomes nonzero if a wait timed out. */
+int zmi_mamba_block(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err, void* stream);
+int64_t zmi_mamba_block_gran_words(int rows, int d_in_proj);
 
 /* ---------------------------------------------------------------------------------------
  * Synthetic weights: fill with the counter-based uniform stream of zonos_vibes_amd/synthetic.py

@@ -120,6 +120,8 @@ _SIGS = {
     "zmi_mamba2_scan": (c_int, [ctypes.POINTER(Mamba2Args), c_int, c_void_p]),
     "zmi_add_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                   c_void_p, c_int, c_int, c_void_p]),
+    "zmi_mamba_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(Mamba2Args), c_void_p, c_void_p, c_void_p]),
+    "zmi_mamba_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_gated_rmsnorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_int,
                                   c_void_p]),
     "zmi_fill_uniform": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_int, c_void_p]),

@@ -130,7 +130,8 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   constexpr int NWV = G * W;
   constexpr int XROW = Img<K>::XROW;
   static_assert(RT == 8 || RT == 16, "row tile");
-  static_assert(!FUSE || EPI == ZMI_EPI_QKV, "only the QKV projection hands off in-launch");
+  static_assert(!FUSE || EPI == ZMI_EPI_QKV || EPI == ZMI_EPI_STORE, "in-launch hand-off: QKV or plain store");
+  static_assert(FUSE != 2 || NTW, "the store hand-off runs on single-tile (decode) launches");
 
   // block -> (column block, group of rpw row tiles): the groups of one column block take ids 8 apart.
   // A workgroup keeps its weight slice in registers and runs its row tiles one after the other, each
@@ -429,7 +430,24 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   };
 
   // (6) fused epilogues
-  if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {
+  if (EPI == ZMI_EPI_STORE && FUSE == 2) {
+    // plain bf16 store, and every column pair of an active row also goes out as an 8-byte {pair,
+    // tag = position + 1} granule (zmi_mamba_block's step role reads the in_proj output from these)
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
+      const bool ok = r < rows && n < a.n_valid;
+      const uint32_t hv = ok ? f2bf(colsum(c, r)) : 0u;
+      const uint32_t nb = (uint32_t)__shfl_down((int)hv, 1);
+      if (ok) {
+        const size_t m = (size_t)(row0 + r);
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)hv;
+        const int pos = a.row_pos[m];
+        if ((c & 1) == 0 && pos >= 0)
+          st_wt64(fz.gran + m * fz.gran_stride + (n >> 1), (uint64_t)(hv | (nb << 16)) | ((uint64_t)(unsigned)(pos + 1) << 32));
+      }
+    }
+  } else if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
       const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;

@@ -21,106 +21,29 @@
 //   ssm state  bf16 [row][nheads][headdim 64][d_state 128] (the reference keeps it in the cache dtype).
 #include "zmi_common.h"
 #include "zmi_kernels.h"
+#include "zmi_mamba_step.h"
 
 namespace {
 
-constexpr int MB_HD = 64;    // headdim
-constexpr int MB_DS = 128;   // d_state (ngroups = 1)
-constexpr int MB_DC = 4;     // d_conv
-constexpr int MB_NT = 256;   // threads: (p = t / 4, n-quarter = t % 4)
-constexpr int MB_NCH = MB_HD + 2 * MB_DS;  // conv channels one head needs: its x, then B, C
+using namespace zmi_mamba;
 
-__device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
-// mamba_ssm/ops/triton/softplus.py; selective_state_update applies it below 20 only
-__device__ __forceinline__ float softplus_f(float v) { return v <= 20.f ? log1pf(expf(v)) : v; }
-
-// xBC channel index of local conv channel i of head h
-__device__ __forceinline__ int conv_channel(int i, int h, int d_ssm) {
-  return i < MB_HD ? h * MB_HD + i : d_ssm + (i - MB_HD);
-}
-
-// causal depthwise conv1d of one channel: bias first, taps oldest first, fp32 (causal_conv1d
-// update / fwd kernels), then SiLU; the caller rounds to bf16 (the conv output tensor is bf16)
-__device__ __forceinline__ float conv4(const bf16_t* w4, float bias, float x0, float x1, float x2, float x3) {
-  float acc = bias;
-  acc = fmaf(bf2f(w4[0]), x0, acc);
-  acc = fmaf(bf2f(w4[1]), x1, acc);
-  acc = fmaf(bf2f(w4[2]), x2, acc);
-  acc = fmaf(bf2f(w4[3]), x3, acc);
-  return silu_f(acc);
-}
-
-// ---------------------------------------------------------------------------- decode step
 __global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args a) {
   const int m = blockIdx.x / a.nheads, h = blockIdx.x - m * a.nheads;
   const int pos = a.row_pos[m];
   if (pos < 0) return;
   const int kv = a.row_kv ? a.row_kv[m] : m;
-  const int conv_dim = a.d_ssm + 2 * MB_DS;
-  const bf16_t* zx = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)m * a.ld_zx;
-  const bf16_t* xin = zx + a.d_ssm;  // z | xBC | dt
-  bf16_t* ring = reinterpret_cast<bf16_t*>(a.conv_ring) + (size_t)kv * MB_DC * conv_dim;
-  const bf16_t* cw = reinterpret_cast<const bf16_t*>(a.conv_w);
-  const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
   __shared__ float xs[MB_HD], bc[2 * MB_DS];
-  const int t = threadIdx.x;
-  // the state slice first: its 64 B per lane are the longest loads, in flight under the conv phase
-  const int p = t >> 2, nq = t & 3;
-  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
-  uint4 sv[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) sv[j] = reinterpret_cast<const uint4*>(st)[j];
-
-  // (1) conv + SiLU of this head's 64 x channels and the 256 B / C channels (every head recomputes
-  // B / C; head 0 alone writes their ring slot)
-  for (int i = t; i < MB_NCH; i += MB_NT) {
-    const int c = conv_channel(i, h, a.d_ssm);
-    float v[MB_DC - 1];
-#pragma unroll
-    for (int k = 0; k < MB_DC - 1; ++k) {
-      const int q = pos - (MB_DC - 1) + k;
-      v[k] = q >= 0 ? bf2f(ring[(size_t)(q & 3) * conv_dim + c]) : 0.f;
-    }
-    const bf16_t raw = xin[c];
-    const float o = bfround(conv4(cw + (size_t)c * MB_DC, bf2f(cb[c]), v[0], v[1], v[2], bf2f(raw)));
-    if (i < MB_HD) xs[i] = o; else bc[i - MB_HD] = o;
-    if (i < MB_HD || h == 0) ring[(size_t)(pos & 3) * conv_dim + c] = raw;
+  __shared__ bf16_t raw[RAW_N];
+  StepPre<MB_NT> pre;
+  step_prefetch<MB_NT>(a, h, pos, kv, pre);  // the state slice first: the longest loads, under the rest
+  const bf16_t* zx = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)m * a.ld_zx;
+  for (int i = threadIdx.x; i < RAW_DT + 1; i += MB_NT) {
+    const int col = i < RAW_Z ? a.d_ssm + conv_channel(i, h, a.d_ssm)
+                              : (i < RAW_DT ? h * MB_HD + (i - RAW_Z) : 2 * a.d_ssm + 2 * MB_DS + h);
+    raw[i] = zx[col];
   }
-  // (2) dt = softplus(dt + dt_bias), dA = exp(A dt)  (selective_state_update, tie_hdim)
-  const float dtv = softplus_f(bf2f(zx[2 * a.d_ssm + 2 * MB_DS + h]) + a.dt_bias[h]);
-  const float dA = expf(a.A[h] * dtv);
   __syncthreads();
-
-  // (3) state update and readout: lane (p, quarter) owns state[p][32 quarter .. +31]
-  const float x = xs[p];
-  const float* B = bc + nq * 32;
-  const float* C = bc + MB_DS + nq * 32;
-  float out = 0.f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint32_t w[4] = {sv[j].x, sv[j].y, sv[j].z, sv[j].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = 8 * j + 2 * e;
-      float s0 = bf2f(w[e]), s1 = bf2f(w[e] >> 16);
-      s0 = s0 * dA + (B[n] * dtv) * x;
-      s1 = s1 * dA + (B[n + 1] * dtv) * x;
-      out += s0 * C[n];
-      out += s1 * C[n + 1];
-      w[e] = f2bf(s0) | (f2bf(s1) << 16);
-    }
-    sv[j] = uint4{w[0], w[1], w[2], w[3]};
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = sv[j];
-  out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
-  if (nq == 0) {
-    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * a.D[h]);
-    if (a.gz) {  // RMSNormGated's gate of this channel, once (the out_proj GEMV's GRMS prologue multiplies)
-      const float zz = bf2f(zx[h * MB_HD + p]);
-      a.gz[(size_t)m * a.ldy + h * MB_HD + p] = zz * (1.0f / (1.0f + expf(-zz)));
-    }
-  }
+  step_core<MB_NT>(a, m, h, pos, kv, raw, pre, xs, bc);
 }
 
 // ---------------------------------------------------------------------------- prefill scan

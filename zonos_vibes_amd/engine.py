@@ -400,7 +400,7 @@ class HipEngine:
             sz = ctypes.sizeof(_lib.Sampling)
             self.params[slot * sz:(slot + 1) * sz].copy_(cp)
             _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
-            self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()  # no granule of an earlier utterance may match a tag
+            self._reset_granules(slot)  # no granule of an earlier utterance may match a tag
             xp = self.x_pre[: 2 * s_len]
             xp[:lc] = cond[0]
             xp[s_len: s_len + lc] = cond[1]
@@ -420,6 +420,10 @@ class HipEngine:
                 st[k][slot] = v
             self._sample(self.logits_pre, noise, 1, slot, 1)
         return s_len
+
+    def _reset_granules(self, slot: int):
+        """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
+        self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
 
     def _prefill_logits(self, s_len: int):
         """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""

@@ -61,6 +61,8 @@ class HybridEngine(HipEngine):
         self.Fm = int(bb.d_intermediate)
         super().__init__(cfg, device, max_slots, max_seqlen, max_prefill)
         self.attn_block = False  # the fused QKV + attention launch needs the LayerNorm prologue
+        # decode in_proj + Mamba2 step as ONE launch (zmi_mamba_block) for <= 16 rows at d_model 2048
+        self.mamba_block = True
 
     def _kv_layers(self) -> int:
         return len(self.attn_idx)
@@ -82,6 +84,7 @@ class HybridEngine(HipEngine):
             self.hm_pre = z(2 * P, max(self.Fm, self.F, 1))
             self.conv_ring = z(nm, R, md["d_conv"], md["conv_dim"])
             self.ssm = z(nm, R, md["nheads"], md["headdim"], md["d_state"])
+            self.mgran = z(nm, R, md["d_in_proj"] // 2, dt=torch.int64)  # zmi_mamba_block hand-off granules
             self.rope = rope_table_neox(self.hd).to(dev)
         self.stream.synchronize()
 
@@ -137,6 +140,10 @@ class HybridEngine(HipEngine):
         self.w = w
         self._build_plan()
 
+    def _reset_granules(self, slot: int):
+        super()._reset_granules(slot)
+        self.mgran[:, 2 * slot: 2 * slot + 2].zero_()
+
     # ------------------------------------------------------------------ launch helpers
     def _addln(self, hid, res, ln, out, m, store=True):
         lib, d, eps, s = self.lib, self.d, self.eps, self.sptr
@@ -169,6 +176,14 @@ class HybridEngine(HipEngine):
         def run():
             _lib.check(lib.zmi_gated_rmsnorm(yp, md["d_ssm"], zp, md["d_in_proj"], m, md["d_ssm"], wp, 1e-5, op,
                                              md["d_ssm"], s), "gated_rmsnorm")
+        return run
+
+    def _call_mamba_block(self, ia, sa, gran):
+        lib, s, ep, gp = self.lib, self.sptr, self.blk_err.data_ptr(), gran.data_ptr()
+        ia.row_pos = sa.row_pos  # the in_proj epilogue tags its granules with the row's position + 1
+
+        def run():
+            _lib.check(lib.zmi_mamba_block(ctypes.byref(ia), ctypes.byref(sa), gp, ep, s), "mamba_block")
         return run
 
     def _call_step(self, a):
@@ -252,13 +267,17 @@ class HybridEngine(HipEngine):
                     plan.append(("attn", j))
                     plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)))
                 else:
-                    plan.append(normed_gemv(self._gemv(lw["in_proj"], x_in, rows, md["d_in_proj"], d, _lib.EPI_STORE,
-                                                       self.zx, md["d_in_proj"]), ln1, i == 0))
+                    inp = normed_gemv(self._gemv(lw["in_proj"], x_in, rows, md["d_in_proj"], d, _lib.EPI_STORE,
+                                                 self.zx, md["d_in_proj"]), ln1, i == 0)
                     sa = self._mamba_args(lw, self.zx, self.yb, rows, self.row_pos, None)
                     fuse_g = rows <= 4  # the f32 gate rows of a larger tile would not fit the LDS image
                     if fuse_g:
                         sa.gz = self.gz.data_ptr()
-                    plan.append(("call", self._call_step(sa)))
+                    if self.mamba_block and d == 2048 and rows <= 16:
+                        plan.append(("call", self._call_mamba_block(inp[1][0], sa, self.mgran[lw["st"]])))
+                    else:
+                        plan.append(inp)
+                        plan.append(("call", self._call_step(sa)))
                     out = self._gemv(lw["out"], self.yb, rows, d, md["d_ssm"], _lib.EPI_STORE, self.hid, d)
                     if fuse_g:
                         out[0].ln_w = lw["norm_w"].data_ptr()
