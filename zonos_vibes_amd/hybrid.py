@@ -7,7 +7,8 @@ hipGraph-captured decode loop, slots — is HipEngine's; this class only swaps t
 
   every block    layer_norm_fn prenorm (residual += hidden in fp32, LayerNorm): decode as the ADDLN
                  prologue of the block's first GEMV, prefill as zmi_add_layernorm (same arithmetic)
-  Mamba2 block   in_proj GEMV -> zmi_mamba2_step (conv ring + SiLU + selective state update)
+  Mamba2 block   zmi_mamba_block: in_proj GEMV + the Mamba2 step (conv ring + SiLU + selective state
+                 update) in one launch, granule hand-off (zmi_mamba2_step as its own launch above 16 rows)
                  -> out_proj GEMV with the GRMS prologue (RMSNormGated; prefill: zmi_gated_rmsnorm and
                  zmi_mamba2_scan over the sequence)
   MHA block      QKV GEMV (non-interleaved rotary as interleaved pairs on permuted q / k rows, bf16
