@@ -203,8 +203,10 @@ int zmi_dac_im2col7(const float* wav, int t, void* col, void* stream);
 int zmi_dac_vq(const float* latents, int t, const float* in_w, const float* in_b, const float* codebooks,
                const float* codebooks_n, const float* codebooks_n2, const float* out_w, const float* out_b,
                int64_t* codes, void* stream);
-/* final Snake'd [T][96] -> conv k7 (96->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441)    */
-int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream);
+/* final Snake'd [T][c_in] -> conv k7 (c_in->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441), on the
+ * MFMA conv kernel: w_pad fp16 [7][32][c_in] (output channel 0 = the filter, 1..31 zero), bias_pad f32 [32]. */
+int zmi_dac_conv_out(const void* x, int t, int c_in, const void* w_pad, const float* bias_pad, float* out,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Prefix conditioner (Zonos.prepare_conditioning, model.py:204-212 -> PrefixConditioner.forward,

@@ -96,8 +96,12 @@ class DACAutoencoder:
                                            w2=conv_w(sd[r + "conv2.weight"]), b2=f32(sd[r + "conv2.bias"])))
                 self.blocks.append(blk)
             self.final_alpha = f32(sd["decoder.snake1.alpha"]).reshape(-1)
-            self.out_w = f32(sd["decoder.conv2.weight"]).reshape(-1)        # [96 * 7]
-            self.out_b = float(sd["decoder.conv2.bias"].float().reshape(-1)[0])
+            w2 = f32(sd["decoder.conv2.weight"])                              # [1][96][7]
+            self.out_w = torch.zeros(7, 32, w2.shape[1], device=self.dev)     # [k][co padded to 32][ci]
+            self.out_w[:, 0, :] = w2[0].t()
+            self.out_w = self.out_w.half().contiguous()
+            self.out_b = torch.zeros(32, device=self.dev)
+            self.out_b[0] = f32(sd["decoder.conv2.bias"]).reshape(-1)[0]
             self.has_encoder = "encoder.conv1.weight" in sd
             if self.has_encoder:
                 self._prepare_encoder(sd, f32, conv_w)
@@ -190,7 +194,7 @@ class DACAutoencoder:
             t = tn
             xin, xalt = xalt, xin
         _lib.check(self.lib.zmi_dac_conv_out(xin.data_ptr(), t, self.blocks[-1]["cout"], self.out_w.data_ptr(),
-                                             self.out_b, out.data_ptr(), self.sptr), "conv_out")
+                                             self.out_b.data_ptr(), out.data_ptr(), self.sptr), "conv_out")
 
     @torch.inference_mode()
     def decode(self, codes: torch.Tensor) -> torch.Tensor:

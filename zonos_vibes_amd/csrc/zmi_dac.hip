@@ -28,6 +28,7 @@ struct ConvArgs {
   f16_t* out_snake;
   const float* alpha;
   float* out_f32;
+  int tanh_c0;  // decoder.conv2: out_f32[t] = tanh(y[t][0]) only (c_out zero-padded to 32 for the MFMA tile)
 };
 
 __device__ __forceinline__ float snake(float y, float a, float inv_a) {
@@ -38,12 +39,35 @@ __device__ __forceinline__ float snake(float y, float a, float inv_a) {
   return y + inv_a * (s * s);  // inv_a = 1 / (a + 1e-9), the reference's reciprocal (modeling_dac.py:97)
 }
 
+// all-zero source for the LDS-DMA lanes whose time row lies outside the input (the conv's zero padding)
+__device__ __attribute__((aligned(64))) uint4 g_conv_zero[4];
+
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds) {
+  // one 1 KiB LDS-DMA piece: lane l's 16 B land at lds + 16 l (wave-uniform base). Not counted by the
+  // compiler: the K loop's explicit vmcnt waits cover it (cdna_hip_programming.md §5 'Async global->LDS')
+  const unsigned ldst =
+      __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) const void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(ldst)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4]
+__device__ __forceinline__ void wait_vm(int n) {
+  if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int WM, int WN>
 __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int co0 = blockIdx.y * (32 * WM) + wm * (16 * WM);
-  const int q0 = blockIdx.x * (32 * WN) + wn * (16 * WN);
   const int kq = (lane >> 4) * 8, lr = lane & 15;
 
   f32x4_t acc[WM][WN];
@@ -52,78 +76,70 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // K loop over (tap, 32-channel step), LDS-tiled: the workgroup's A tile [32 WM co][32 ci] and
-  // B tile [32 WN t][32 ci] are fetched once per step as coalesced 64-B row segments (4 lanes per
-  // row), double-buffered in LDS (row stride 80 B: the 16-row fragment reads hit distinct banks),
-  // with the next step's global loads in flight while this step's MFMAs run.
-  constexpr int BM = 32 * WM, BN = 32 * WN, KP = 40;
-  constexpr int NA = (BM * 4 + 255) / 256, NB = (BN * 4 + 255) / 256;
-  // one LDS block: the double-buffered A/B tiles during the K loop, then (reused) the fp32 output
-  // half-tile [BN/2][BM+4] of the epilogue
-  constexpr int AB_BYTES = 2 * (BM + BN) * KP * 2, TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
-  __shared__ __attribute__((aligned(16))) char lds_raw[AB_BYTES > TILE_BYTES ? AB_BYTES : TILE_BYTES];
-  f16_t(&As)[2][BM][KP] = *reinterpret_cast<f16_t(*)[2][BM][KP]>(lds_raw);
-  f16_t(&Bs)[2][BN][KP] = *reinterpret_cast<f16_t(*)[2][BN][KP]>(lds_raw + 2 * BM * KP * 2);
+  // K loop over (tap, 32-channel step). Each step's A tile [BM co][32 ci] and B tile [BN t][32 ci] (64-B
+  // rows) are copied global -> LDS by LDS-DMA, no register staging, into a 3-deep ring: the copies of step
+  // st + 2 are issued while step st's MFMAs run, and a wave waits (counted vmcnt) only for its own pieces of
+  // step st before the barrier that publishes them. The DMA writes lane-linearly (16 rows x 64 B per
+  // piece), so the bank-conflict swizzle sits on the SOURCE: LDS chunk c' of row r holds channel chunk
+  // c' ^ ((r >> 2) & 3), and the fragment reads apply the same XOR (16 lanes, rows r0..r0+15, one chunk:
+  // 16 distinct 16-B slots of the 256-B bank row).
+  constexpr int BM = 32 * WM, BN = 32 * WN, NS = 3;
+  constexpr int NPA = BM / 16, NP = (BM + BN) / 16;  // 1 KiB pieces per step
+  constexpr int STAGE = (BM + BN) * 64, TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
+  constexpr int LDS_BYTES = NS * STAGE > TILE_BYTES ? NS * STAGE : TILE_BYTES;
+  __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];
   float(&tile)[BN / 2][TP] = *reinterpret_cast<float(*)[BN / 2][TP]>(lds_raw);
-  const int tid = threadIdx.x;
   const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
   const int nci = a.c_in / 32, nsteps = a.taps * nci;
-  uint4 ra[NA], rb[NB];
-#define ZMI_CONV_GLOAD(st_)                                                                               \
-  do {                                                                                                    \
-    const int tap_ = (st_) / nci, ci_ = ((st_) - tap_ * nci) * 32;                                         \
-    _Pragma("unroll") for (int r = 0; r < NA; ++r) {                                                      \
-      const int e = tid + 256 * r;                                                                        \
-      if ((BM * 4) % 256 == 0 || e < BM * 4)                                                              \
-        ra[r] = *reinterpret_cast<const uint4*>(a.w + ((size_t)tap_ * a.c_out + co_blk + (e >> 2)) * a.c_in + \
-                                                ci_ + (e & 3) * 8);                                        \
-    }                                                                                                     \
-    _Pragma("unroll") for (int r = 0; r < NB; ++r) {                                                      \
-      const int e = tid + 256 * r;                                                                        \
-      if ((BN * 4) % 256 == 0 || e < BN * 4) {                                                            \
-        const int q = q_blk + (e >> 2);                                                                   \
-        const int tin = q + a.in_off + tap_ * a.tap_step;                                                 \
-        const bool ok = q < a.n_out && tin >= 0 && tin < a.t_in;                                          \
-        rb[r] = ok ? *reinterpret_cast<const uint4*>(a.x + (size_t)tin * a.c_in + ci_ + (e & 3) * 8)      \
-                   : uint4{0u, 0u, 0u, 0u};                                                               \
-      }                                                                                                   \
-    }                                                                                                     \
-  } while (0)
-#define ZMI_CONV_LSTORE(buf_)                                                                             \
-  do {                                                                                                    \
-    _Pragma("unroll") for (int r = 0; r < NA; ++r) {                                                      \
-      const int e = tid + 256 * r;                                                                        \
-      if ((BM * 4) % 256 == 0 || e < BM * 4) *reinterpret_cast<uint4*>(&As[buf_][e >> 2][(e & 3) * 8]) = ra[r]; \
-    }                                                                                                     \
-    _Pragma("unroll") for (int r = 0; r < NB; ++r) {                                                      \
-      const int e = tid + 256 * r;                                                                        \
-      if ((BN * 4) % 256 == 0 || e < BN * 4) *reinterpret_cast<uint4*>(&Bs[buf_][e >> 2][(e & 3) * 8]) = rb[r]; \
-    }                                                                                                     \
-  } while (0)
+  const int npw = (NP - wave + 3) / 4;  // this wave's pieces per step: p = wave, wave + 4, ...
+  // per-lane piece geometry: row 16 p + (lane >> 2), LDS chunk lane & 3, source chunk swizzled
+  const int prow = lane >> 2, pchunk = (lane & 3) ^ ((lane >> 4) & 3);
+  auto issue = [&](int st_) {
+    const int tap_ = st_ / nci, ci_ = (st_ - tap_ * nci) * 32 + pchunk * 8;
+    char* stg = lds_raw + (st_ % NS) * STAGE;
+#pragma unroll
+    for (int k = 0; k < (NP + 3) / 4; ++k) {
+      const int p = wave + 4 * k;
+      if (p < NP) {
+        const void* src;
+        if (p < NPA) {
+          src = a.w + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_;
+        } else {
+          const int q = q_blk + 16 * (p - NPA) + prow;
+          const int tin = q + a.in_off + tap_ * a.tap_step;
+          const bool ok = q < a.n_out && tin >= 0 && tin < a.t_in;
+          src = ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3];
+        }
+        glds16(src, stg + p * 1024);
+      }
+    }
+  };
   const int am = wm * (16 * WM), bn = wn * (16 * WN);
-  ZMI_CONV_GLOAD(0);
-  ZMI_CONV_LSTORE(0);
-  __syncthreads();
+  const int rslot = ((lane >> 4) ^ ((lr >> 2) & 3)) * 16;  // swizzled byte offset of this lane's fragment
+  issue(0);
+  if (nsteps > 1) issue(1);
   for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) ZMI_CONV_GLOAD(st + 1);
+    wait_vm(st + 1 < nsteps ? npw : 0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + 2 < nsteps) issue(st + 2);
+    const char* stg = lds_raw + (st % NS) * STAGE;
     uint4 af[WM], bfr[WN];
 #pragma unroll
-    for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const uint4*>(&As[buf][am + i * 16 + lr][kq]);
+    for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const uint4*>(stg + (am + i * 16 + lr) * 64 + rslot);
 #pragma unroll
-    for (int j = 0; j < WN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(&Bs[buf][bn + j * 16 + lr][kq]);
+    for (int j = 0; j < WN; ++j)
+      bfr[j] = *reinterpret_cast<const uint4*>(stg + BM * 64 + (bn + j * 16 + lr) * 64 + rslot);
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
       for (int j = 0; j < WN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, af[i]),
                                                            __builtin_bit_cast(f16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
-    if (st + 1 < nsteps) ZMI_CONV_LSTORE(buf ^ 1);
-    __syncthreads();
+    asm volatile("" ::: "memory");
   }
-
-#undef ZMI_CONV_GLOAD
-#undef ZMI_CONV_LSTORE
+  __syncthreads();  // every wave's last fragment reads are done before the ring is reused as the output tile
+  const int tid = threadIdx.x;
   // epilogue, in two halves of the time tile (the waves with wn == half own it): the accumulators go
   // through LDS as an fp32 [t][co] tile, then every thread finishes 8 consecutive channels of one
   // time row, so the skip loads and the raw / snake / f32 stores are whole 16-32 B per lane and
@@ -165,7 +181,9 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
           o.w = f2h(y[6]) | (f2h(y[7]) << 16);
           *reinterpret_cast<uint4*>(a.out_raw + to * a.c_out + co) = o;
         }
-        if (a.out_f32) {
+        if (a.tanh_c0) {
+          if (co == 0) a.out_f32[to] = tanhf(y[0]);
+        } else if (a.out_f32) {
           float4* dst = reinterpret_cast<float4*>(a.out_f32 + to * a.c_out + co);
           dst[0] = float4{y[0], y[1], y[2], y[3]};
           dst[1] = float4{y[4], y[5], y[6], y[7]};
@@ -213,29 +231,6 @@ __global__ __launch_bounds__(256) void from_codes_kernel(const int64_t* codes, i
     }
     z[(size_t)t * 1024 + c] = (f16_t)f2h(acc);
   }
-}
-
-// decoder.conv2 (96 -> 1, k7, pad 3) + tanh (modeling_dac.py:438-441); input already Snake'd
-__global__ __launch_bounds__(256) void conv_out_kernel(const f16_t* x, int T, int c_in, const float* w, float bias,
-                                                        float* out) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= T) return;
-  float acc = 0.f;
-  for (int k = 0; k < 7; ++k) {
-    const int ti = t + k - 3;
-    if (ti < 0 || ti >= T) continue;
-    const f16_t* xr = x + (size_t)ti * c_in;
-    for (int c = 0; c < c_in; c += 8) {
-      const uint4 v = *reinterpret_cast<const uint4*>(xr + c);
-      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc += w[(c + 2 * j) * 7 + k] * h2f(u[j]);
-        acc += w[(c + 2 * j + 1) * 7 + k] * h2f(u[j] >> 16);
-      }
-    }
-  }
-  out[t] = tanhf(acc + bias);
 }
 
 // encoder.conv1 input (modeling_dac.py:451, Conv1d(1, 64, k7, pad 3)) as a 32-channel im2col row per
@@ -405,7 +400,7 @@ extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, co
   if (n_out <= 0) return 0;
   if ((size_t)(n_out - 1) * out_stride + out_phase >= (size_t)t_out) return zmi_fail_msg("dac_conv: output bounds");
   ConvArgs a{(const f16_t*)x, t_in, c_in, (const f16_t*)w, bias, c_out, taps, tap_step, in_off, n_out,
-             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha, out_f32};
+             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha, out_f32, 0};
   hipStream_t s = (hipStream_t)stream;
   // 128-step time tiles: 64- and 32-step tiles measured 15 % and 65 % slower (more workgroups do
   // not hide the per-K-step load latency)
@@ -415,10 +410,16 @@ extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, co
   return 0;
 }
 
-extern "C" int zmi_dac_conv_out(const void* x, int t, int c_in, const float* w, float bias, float* out, void* stream) {
-  if (c_in % 8) return zmi_fail_msg("dac_conv_out: c_in % 8");
-  hipLaunchKernelGGL(conv_out_kernel, dim3((t + 255) / 256), dim3(256), 0, (hipStream_t)stream, (const f16_t*)x, t,
-                     c_in, w, bias, out);
+extern "C" int zmi_dac_conv_out(const void* x, int t, int c_in, const void* w_pad, const float* bias_pad, float* out,
+                                void* stream) {
+  // decoder.conv2 (c_in -> 1, k7, pad 3) + tanh (modeling_dac.py:438-441) on the MFMA conv kernel: w_pad is
+  // [7][32][c_in] fp16 with output channel 0 the real filter and 1..31 zero, bias_pad [32]; x already Snake'd
+  if (c_in % 32) return zmi_fail_msg("dac_conv_out: c_in % 32");
+  if (t <= 0) return 0;
+  ConvArgs a{(const f16_t*)x, t, c_in, (const f16_t*)w_pad, bias_pad, 32, 7, 1, -3, t, 1, 0, t,
+             nullptr, nullptr, nullptr, nullptr, out, 1};
+  const int rc = launch_conv<4>(a, (hipStream_t)stream);
+  if (rc) return rc;
   ZMI_CHECK(hipGetLastError());
   return 0;
 }
