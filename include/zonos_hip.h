@@ -203,6 +203,11 @@ int zmi_dac_im2col7(const float* wav, int t, void* col, void* stream);
 int zmi_dac_vq(const float* latents, int t, const float* in_w, const float* in_b, const float* codebooks,
                const float* codebooks_n, const float* codebooks_n2, const float* out_w, const float* out_b,
                int64_t* codes, void* stream);
+/* polyphase ConvTranspose1d(c_in, c_out, k = 2 stride, stride, pad) of a DacDecoderBlock (modeling_dac.py:222-240),
+ * every phase in one launch: w_phases fp16 [stride][2][c_out][c_in], phase rho's taps (rho + pad) % stride and
+ * + stride, transposed; out [stride t_in][c_out] raw and / or Snake'd with alpha. */
+int zmi_dac_conv_t(const void* x, int t_in, int c_in, const void* w_phases, const float* bias, int c_out, int stride,
+                   int pad, void* out_raw, void* out_snake, const float* alpha, void* stream);
 /* final Snake'd [T][c_in] -> conv k7 (c_in->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441), on the
  * MFMA conv kernel: w_pad fp16 [7][32][c_in] (output channel 0 = the filter, 1..31 zero), bias_pad f32 [32]. */
 int zmi_dac_conv_out(const void* x, int t, int c_in, const void* w_pad, const float* bias_pad, float* out,

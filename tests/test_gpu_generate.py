@@ -232,7 +232,8 @@ def test_dac_decode_matches_reference():
     err = (wav - ref).abs()
     snr = 10 * torch.log10(ref.pow(2).mean() / (wav - ref).pow(2).mean())
     # fp16 activations / fp32 accumulation vs the fp32 CPU reference (the reference GPU path is fp16 autocast)
-    assert err.max() < 2e-2 and snr > 35, (err.max().item(), snr.item())
+    print(f"dac decode max-abs {err.max().item():.3e} snr {snr.item():.1f} dB")
+    assert err.max() < 2e-3 and snr > 50, (err.max().item(), snr.item())  # measured 2.1e-4, 59 dB
 
 
 def test_generate_is_deterministic(traj):

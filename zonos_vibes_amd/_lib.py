@@ -113,6 +113,8 @@ _SIGS = {
     "zmi_dac_im2col7": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "zmi_dac_vq": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p]),
+    "zmi_dac_conv_t": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                c_void_p, c_void_p]),
     "zmi_dac_conv_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_prefix_condition": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_float,
                                      c_void_p, c_void_p]),

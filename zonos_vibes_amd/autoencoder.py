@@ -82,12 +82,12 @@ class DACAutoencoder:
                 wt = sd[p + "conv_t1.weight"].to(self.dev, torch.float32)  # [cin][cout][2s]
                 pad = math.ceil(s / 2)
                 phases = []
-                for rho in range(s):
+                for rho in range(s):  # polyphase: phase rho uses taps (rho + pad) % s and + s, transposed
                     k0 = (rho + pad) % s
-                    taps = torch.stack([wt[:, :, k0].t(), wt[:, :, k0 + s].t()])  # [2][cout][cin]
-                    phases.append((taps.contiguous().half(), (rho + pad) // s))
-                blk = dict(stride=s, cin=wt.shape[0], cout=wt.shape[1], alpha=f32(sd[p + "snake1.alpha"]).reshape(-1),
-                           phases=phases, bt=f32(sd[p + "conv_t1.bias"]), res=[])
+                    phases.append(torch.stack([wt[:, :, k0].t(), wt[:, :, k0 + s].t()]))  # [2][cout][cin]
+                blk = dict(stride=s, pad=pad, cin=wt.shape[0], cout=wt.shape[1],
+                           alpha=f32(sd[p + "snake1.alpha"]).reshape(-1),
+                           wt=torch.stack(phases).half().contiguous(), bt=f32(sd[p + "conv_t1.bias"]), res=[])
                 for u in range(3):
                     r = p + f"res_unit{u + 1}."
                     blk["res"].append(dict(a1=f32(sd[r + "snake1.alpha"]).reshape(-1),
@@ -175,9 +175,10 @@ class DACAutoencoder:
             s, cin, cout = blk["stride"], blk["cin"], blk["cout"]
             tn = t * s
             res = blk["res"]
-            for rho, (wp, coff) in enumerate(blk["phases"]):  # polyphase ConvTranspose1d(k=2s, s, pad=ceil(s/2))
-                self._conv(xin, t, cin, wp, blk["bt"], cout, 2, -1, coff, t, s, rho, tn, raw=H, snake=xalt,
-                           alpha=res[0]["a1"])
+            # ConvTranspose1d(k=2s, s, pad=ceil(s/2)), every phase in one launch
+            _lib.check(self.lib.zmi_dac_conv_t(xin.data_ptr(), t, cin, blk["wt"].data_ptr(), blk["bt"].data_ptr(),
+                                               cout, s, blk["pad"], H.data_ptr(), xalt.data_ptr(),
+                                               res[0]["a1"].data_ptr(), self.sptr), "dac_conv_t")
             for u, dil in enumerate(DILATIONS):
                 ru = res[u]
                 self._conv(xalt, tn, cout, ru["w1"], ru["b1"], cout, 7, dil, -3 * dil, tn, 1, 0, tn, snake=S2,

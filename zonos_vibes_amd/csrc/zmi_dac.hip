@@ -29,6 +29,11 @@ struct ConvArgs {
   const float* alpha;
   float* out_f32;
   int tanh_c0;  // decoder.conv2: out_f32[t] = tanh(y[t][0]) only (c_out zero-padded to 32 for the MFMA tile)
+  // polyphase ConvTranspose as ONE launch (blockIdx.z = phase rho, nphase = stride): phase rho reads its
+  // own [taps][c_out][c_in] weights at w + rho * w_phase, in_off = (rho + phase_pad) / out_stride,
+  // out_phase = rho. nphase == 1: in_off / out_phase / w as given.
+  int nphase, phase_pad;
+  size_t w_phase;
 };
 
 __device__ __forceinline__ float snake(float y, float a, float inv_a) {
@@ -55,16 +60,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds) {
                : "memory");
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 4]
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 12]
 __device__ __forceinline__ void wait_vm(int n) {
-  if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  switch (n) {
+#define ZMI_WAIT_VM(k_) \
+  case k_: asm volatile("s_waitcnt vmcnt(" #k_ ")" ::: "memory"); break;
+    ZMI_WAIT_VM(1) ZMI_WAIT_VM(2) ZMI_WAIT_VM(3) ZMI_WAIT_VM(4) ZMI_WAIT_VM(5) ZMI_WAIT_VM(6)
+    ZMI_WAIT_VM(7) ZMI_WAIT_VM(8) ZMI_WAIT_VM(9) ZMI_WAIT_VM(10) ZMI_WAIT_VM(11) ZMI_WAIT_VM(12)
+#undef ZMI_WAIT_VM
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int NS>
 __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -77,19 +85,23 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // K loop over (tap, 32-channel step). Each step's A tile [BM co][32 ci] and B tile [BN t][32 ci] (64-B
-  // rows) are copied global -> LDS by LDS-DMA, no register staging, into a 3-deep ring: the copies of step
-  // st + 2 are issued while step st's MFMAs run, and a wave waits (counted vmcnt) only for its own pieces of
-  // step st before the barrier that publishes them. The DMA writes lane-linearly (16 rows x 64 B per
+  // rows) are copied global -> LDS by LDS-DMA, no register staging, into an NS-deep ring: the copies of step
+  // st + NS - 1 are issued while step st's MFMAs run, and a wave waits (counted vmcnt) only for its own
+  // pieces of step st before the barrier that publishes them. The DMA writes lane-linearly (16 rows x 64 B per
   // piece), so the bank-conflict swizzle sits on the SOURCE: LDS chunk c' of row r holds channel chunk
   // c' ^ ((r >> 2) & 3), and the fragment reads apply the same XOR (16 lanes, rows r0..r0+15, one chunk:
   // 16 distinct 16-B slots of the 256-B bank row).
-  constexpr int BM = 32 * WM, BN = 32 * WN, NS = 3;
+  constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int NPA = BM / 16, NP = (BM + BN) / 16;  // 1 KiB pieces per step
   constexpr int STAGE = (BM + BN) * 64, TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
   constexpr int LDS_BYTES = NS * STAGE > TILE_BYTES ? NS * STAGE : TILE_BYTES;
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];
   float(&tile)[BN / 2][TP] = *reinterpret_cast<float(*)[BN / 2][TP]>(lds_raw);
   const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
+  const int rho = blockIdx.z;
+  const f16_t* const wts = a.w + (size_t)rho * a.w_phase;
+  const int in_off = a.nphase > 1 ? (rho + a.phase_pad) / a.out_stride : a.in_off;
+  const int out_phase = a.nphase > 1 ? rho : a.out_phase;
   const int nci = a.c_in / 32, nsteps = a.taps * nci;
   const int npw = (NP - wave + 3) / 4;  // this wave's pieces per step: p = wave, wave + 4, ...
   // per-lane piece geometry: row 16 p + (lane >> 2), LDS chunk lane & 3, source chunk swizzled
@@ -103,10 +115,10 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
       if (p < NP) {
         const void* src;
         if (p < NPA) {
-          src = a.w + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_;
+          src = wts + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_;
         } else {
           const int q = q_blk + 16 * (p - NPA) + prow;
-          const int tin = q + a.in_off + tap_ * a.tap_step;
+          const int tin = q + in_off + tap_ * a.tap_step;
           const bool ok = q < a.n_out && tin >= 0 && tin < a.t_in;
           src = ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3];
         }
@@ -116,13 +128,15 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   };
   const int am = wm * (16 * WM), bn = wn * (16 * WN);
   const int rslot = ((lane >> 4) ^ ((lr >> 2) & 3)) * 16;  // swizzled byte offset of this lane's fragment
-  issue(0);
-  if (nsteps > 1) issue(1);
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < nsteps) issue(k);
   for (int st = 0; st < nsteps; ++st) {
-    wait_vm(st + 1 < nsteps ? npw : 0);
+    // outstanding after step st's pieces: those of steps st + 1 .. st + NS - 2 that were issued
+    wait_vm(npw * (min(nsteps - 1, st + NS - 2) - st));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 2 < nsteps) issue(st + 2);
+    if (st + NS - 1 < nsteps) issue(st + NS - 1);
     const char* stg = lds_raw + (st % NS) * STAGE;
     uint4 af[WM], bfr[WN];
 #pragma unroll
@@ -161,7 +175,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
       const int q = q_blk + half * ROWS + row;
       if (q < a.n_out) {
         const int co = co_blk + c8 * 8;
-        const size_t to = (size_t)q * a.out_stride + a.out_phase;
+        const size_t to = (size_t)q * a.out_stride + out_phase;
         const f32x4_t v0 = *reinterpret_cast<const f32x4_t*>(&tile[row][c8 * 8]);
         const f32x4_t v1 = *reinterpret_cast<const f32x4_t*>(&tile[row][c8 * 8 + 4]);
         float y[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
@@ -377,18 +391,31 @@ extern "C" int zmi_dac_from_codes(const int64_t* codes, int T, const float* code
   return 0;
 }
 
-template <int WN>
+// Tile height: the largest BM = 32 WM (WM in 4, 3, 2, 1, dividing c_out) whose grid still gives every CU
+// about two workgroups; the early, few-frame stages (conv1 and block 0 at 861 frames: 84-336 workgroups at
+// BM = 128) are latency-bound per workgroup, so more, shorter tiles finish sooner there.
 static int launch_conv(const ConvArgs& a, hipStream_t s) {
-  const int bn = 32 * WN;
-  if (a.c_out % 128 == 0) {
-    hipLaunchKernelGGL((conv_kernel<4, WN>), dim3((a.n_out + bn - 1) / bn, a.c_out / 128), dim3(256), 0, s, a);
-  } else if (a.c_out % 96 == 0) {
-    hipLaunchKernelGGL((conv_kernel<3, WN>), dim3((a.n_out + bn - 1) / bn, a.c_out / 96), dim3(256), 0, s, a);
-  } else if (a.c_out % 32 == 0) {
-    hipLaunchKernelGGL((conv_kernel<1, WN>), dim3((a.n_out + bn - 1) / bn, a.c_out / 32), dim3(256), 0, s, a);
-  } else {
-    return zmi_fail_msg("dac_conv: c_out must be a multiple of 32");
+  constexpr int WN = 4, BN = 32 * WN;
+  const unsigned nq = (unsigned)((a.n_out + BN - 1) / BN), nz = (unsigned)a.nphase;
+  const int want = 256;
+  int wm = 0;
+  for (int c : {4, 3, 2, 1})
+    if (a.c_out % (32 * c) == 0) {
+      wm = c;
+      if ((long)nq * nz * (a.c_out / (32 * c)) >= want) break;
+    }
+  if (!wm) return zmi_fail_msg("dac_conv: c_out must be a multiple of 32");
+  const dim3 grid(nq, (unsigned)(a.c_out / (32 * wm)), nz);
+  // ring depth 2: measured against 3 and 4 (3.60 / 3.74 / 4.14 ms DAC decode at 861 frames): the deeper
+  // rings' LDS costs more than their extra step of load lookahead gains
+#define ZMI_CONV_L(wm_) hipLaunchKernelGGL((conv_kernel<wm_, WN, 2>), grid, dim3(256), 0, s, a)
+  switch (wm) {
+    case 4: ZMI_CONV_L(4); break;
+    case 3: ZMI_CONV_L(3); break;
+    case 2: ZMI_CONV_L(2); break;
+    default: ZMI_CONV_L(1); break;
   }
+#undef ZMI_CONV_L
   return 0;
 }
 
@@ -400,11 +427,11 @@ extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, co
   if (n_out <= 0) return 0;
   if ((size_t)(n_out - 1) * out_stride + out_phase >= (size_t)t_out) return zmi_fail_msg("dac_conv: output bounds");
   ConvArgs a{(const f16_t*)x, t_in, c_in, (const f16_t*)w, bias, c_out, taps, tap_step, in_off, n_out,
-             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha, out_f32, 0};
+             out_stride, out_phase, t_out, (const f16_t*)skip, (f16_t*)out_raw, (f16_t*)out_snake, alpha, out_f32, 0, 1, 0, 0};
   hipStream_t s = (hipStream_t)stream;
   // 128-step time tiles: 64- and 32-step tiles measured 15 % and 65 % slower (more workgroups do
   // not hide the per-K-step load latency)
-  const int rc = launch_conv<4>(a, s);
+  const int rc = launch_conv(a, s);
   if (rc) return rc;
   ZMI_CHECK(hipGetLastError());
   return 0;
@@ -417,8 +444,26 @@ extern "C" int zmi_dac_conv_out(const void* x, int t, int c_in, const void* w_pa
   if (c_in % 32) return zmi_fail_msg("dac_conv_out: c_in % 32");
   if (t <= 0) return 0;
   ConvArgs a{(const f16_t*)x, t, c_in, (const f16_t*)w_pad, bias_pad, 32, 7, 1, -3, t, 1, 0, t,
-             nullptr, nullptr, nullptr, nullptr, out, 1};
-  const int rc = launch_conv<4>(a, (hipStream_t)stream);
+             nullptr, nullptr, nullptr, nullptr, out, 1, 1, 0, 0};
+  const int rc = launch_conv(a, (hipStream_t)stream);
+  if (rc) return rc;
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int zmi_dac_conv_t(const void* x, int t_in, int c_in, const void* w_phases, const float* bias, int c_out,
+                              int stride, int pad, void* out_raw, void* out_snake, const float* alpha, void* stream) {
+  // ConvTranspose1d(c_in, c_out, k = 2 stride, stride, padding = pad) (modeling_dac.py:222-240) in polyphase
+  // form, all phases in one launch: out[stride q + rho] = bias + W_rho[0] x[q + c] + W_rho[1] x[q + c - 1],
+  // c = (rho + pad) / stride; w_phases fp16 [stride][2][c_out][c_in] (W_rho[j] = w[:, :, (rho + pad) % stride
+  // + j stride]^T); output length stride * t_in
+  if (c_in % 32) return zmi_fail_msg("dac_conv_t: c_in % 32");
+  if (t_in <= 0) return 0;
+  if (stride < 1 || pad < 0) return zmi_fail_msg("dac_conv_t: stride >= 1, pad >= 0");
+  ConvArgs a{(const f16_t*)x, t_in, c_in, (const f16_t*)w_phases, bias, c_out, 2, -1, 0, t_in, stride, 0,
+             stride * t_in, nullptr, (f16_t*)out_raw, (f16_t*)out_snake, alpha, nullptr, 0, stride, pad,
+             (size_t)2 * c_out * c_in};
+  const int rc = launch_conv(a, (hipStream_t)stream);
   if (rc) return rc;
   ZMI_CHECK(hipGetLastError());
   return 0;
