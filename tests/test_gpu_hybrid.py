@@ -348,3 +348,26 @@ def test_mamba_block_launch_bit_identical_to_separate():
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+def test_attn_block_addln_bit_identical_to_separate():
+    """The MHA blocks' QKV (ADDLN prologue) + attention as one zmi_attn_block launch decode exactly as the
+    separate QKV GEMV + attention kernel: one utterance (2 rows) and 8 slots (16 rows) at full width."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = hybrid_config(2048, 3, [1], 16, 4)
+    m = Zonos.synthetic(cfg, DEV, seed=5, max_slots=8, max_seqlen=96, max_prefill=32)
+    conds = [_bf(2, lc, 2048, seed=80 + lc).to(DEV) for lc in (5, 9, 7, 12, 6, 8, 11, 10)]
+    sp = dict(temperature=0.0)
+    res = []
+    for fused in (True, False):
+        m.engine.attn_block = fused
+        m.engine._build_plan()
+        assert any(it[0] == "attnblk" for it in m.engine._plan(2)) == fused
+        one = m.generate(conds[0], max_new_tokens=30, sampling_params=sp, progress_bar=False)
+        many = m.generate_batch(conds, max_new_tokens=[20, 14, 30, 9, 25, 17, 12, 22], sampling_params=sp,
+                                seeds=list(range(8)), max_slots=8)
+        m.engine.check_errors()
+        res.append((one.cpu(), [c.cpu() for c in many]))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)

@@ -462,14 +462,16 @@ __device__ __forceinline__ void prefetch_body(const ZmiPrefetch& pf, int j, int 
   if (acc == 0x9E3779B9u && pf.sink) *pf.sink = acc;  // keeps the loads; the sink is never read
 }
 
-template <int S>
+// PRO: the projection's prologue, LayerNorm (transformer blocks) or ADDLN (the hybrid's MHA blocks:
+// layer_norm_fn(hidden, residual) with the new residual written by column block 0)
+template <int S, int PRO>
 __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
                                                         int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int n_xs = (n_units + 7) / 8 * 8 * S;
   if (b < n_qkv)
-    zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_LN, ZMI_EPI_QKV, 1, 1>(
+    zmi_gemv::gemv_body<QG, QW, QNL, QRT, PRO, ZMI_EPI_QKV, 1, 1>(
         qa, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, GRAN_STRIDE});
   else if (b < n_qkv + n_xs)
     xs_body<S>(at, n_units, b - n_qkv, smem, gran);
@@ -477,23 +479,23 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
     prefetch_body(pf, b - n_qkv - n_xs, n_pf);
 }
 
-template <int S>
+template <int S, int PRO>
 hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArgs& at, int n_units, uint64_t* gran,
                         const ZmiPrefetch& pf, hipStream_t s) {
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
-  const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, true), XsImg<S>::BYTES,
+  const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, PRO), XsImg<S>::BYTES,
                                zmi_gemv::LDS_MAX / 2 + 1024});
   if (lds > zmi_gemv::LDS_MAX) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S>),
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S, PRO>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)zmi_gemv::LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
   const int n_xs = (n_units + 7) / 8 * 8 * S;
   const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
-  hipLaunchKernelGGL(attn_block_kernel<S>, dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
+  hipLaunchKernelGGL((attn_block_kernel<S, PRO>), dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
                      n_units, gran, pf, n_pf);
   return hipGetLastError();
 }
@@ -508,6 +510,10 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
                                  const ZmiPrefetch* prefetch, void* stream) {
   const ZmiGemvArgs& a = *qkv;
   if (a.K != 2048 || !a.ln_w) return zmi_fail_msg("attn_block: the QKV projection must be LayerNorm'd with K = 2048");
+  const bool addln = a.pro == ZMI_PRO_ADDLN;
+  if (a.pro != ZMI_PRO_AUTO && !addln) return zmi_fail_msg("attn_block: prologue must be LayerNorm or ADDLN");
+  if (addln && (!a.ln_b || !a.aux || a.ld_aux % 8 || a.res_out == a.aux))
+    return zmi_fail_msg("attn_block: ADDLN needs ln_b, the residual rows (ld_aux % 8) and a separate res_out");
   if (a.M < 1 || a.M > QRT) return zmi_fail_msg("attn_block: 1 <= M <= 16 rows (one row tile)");
   if (a.hd != HD || a.hkv <= 0 || a.hq != XG * a.hkv)
     return zmi_fail_msg("attn_block: head_dim 128, 4 query heads per kv head");
@@ -545,11 +551,15 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  switch (slices) {
-    case 4: e = launch_block<4>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s); break;
-    case 8: e = launch_block<8>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s); break;
-    default: return zmi_fail_msg("attn_block: slices must be 4 or 8");
-  }
+  using zmi_gemv::PRO_ADDLN;
+  using zmi_gemv::PRO_LN;
+  if (slices != 4 && slices != 8) return zmi_fail_msg("attn_block: slices must be 4 or 8");
+  if (addln)
+    e = slices == 4 ? launch_block<4, PRO_ADDLN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
+                    : launch_block<8, PRO_ADDLN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s);
+  else
+    e = slices == 4 ? launch_block<4, PRO_LN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
+                    : launch_block<8, PRO_LN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s);
   ZMI_CHECK(e);
   return 0;
 }

@@ -61,7 +61,8 @@ class HybridEngine(HipEngine):
         self.attn_idx = sorted(int(i) for i in bb.attn_layer_idx)
         self.Fm = int(bb.d_intermediate)
         super().__init__(cfg, device, max_slots, max_seqlen, max_prefill)
-        self.attn_block = False  # the fused QKV + attention launch needs the LayerNorm prologue
+        # the MHA blocks' QKV + attention as ONE launch (zmi_attn_block with the ADDLN projection prologue)
+        self.attn_block = True
         # decode in_proj + Mamba2 step as ONE launch (zmi_mamba_block) for <= 16 rows at d_model 2048
         self.mamba_block = True
 
@@ -262,10 +263,18 @@ class HybridEngine(HipEngine):
                 if lw["kind"] == "attn":
                     j = lw["kv"]
                     qkv_n = (self.H + 2 * self.Hkv) * self.hd
-                    plan.append(normed_gemv(self._gemv(lw["qkv"], x_in, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                                       kv=(self.kc[j], self.vc[j]), row_kv=self.row_kv,
-                                                       row_pos=self.row_pos), ln1, i == 0))
-                    plan.append(("attn", j))
+                    qkv = normed_gemv(self._gemv(lw["qkv"], x_in, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                                 kv=(self.kc[j], self.vc[j]), row_kv=self.row_kv,
+                                                 row_pos=self.row_pos), ln1, i == 0)
+                    if self._use_attn_block(rows):
+                        pf = _lib.Prefetch()
+                        if self.prefetch_blocks > 0:  # out_proj's weights into the Infinity Cache meanwhile
+                            pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
+                            pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
+                        plan.append(("attnblk", (qkv[1][0], j, pf)))
+                    else:
+                        plan.append(qkv)
+                        plan.append(("attn", j))
                     plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)))
                 else:
                     inp = normed_gemv(self._gemv(lw["in_proj"], x_in, rows, md["d_in_proj"], d, _lib.EPI_STORE,
