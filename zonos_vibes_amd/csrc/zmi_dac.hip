@@ -72,7 +72,9 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
-template <int WM, int WN, int NS>
+constexpr int HALO_PIECES = 12;  // the halo K order's activation tile: up to 192 rows = BN + 64 rows of taps
+
+template <int WM, int WN, int NS, bool HALO>
 __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -84,17 +86,24 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // K loop over (tap, 32-channel step). Each step's A tile [BM co][32 ci] and B tile [BN t][32 ci] (64-B
-  // rows) are copied global -> LDS by LDS-DMA, no register staging, into an NS-deep ring: the copies of step
-  // st + NS - 1 are issued while step st's MFMAs run, and a wave waits (counted vmcnt) only for its own
-  // pieces of step st before the barrier that publishes them. The DMA writes lane-linearly (16 rows x 64 B per
-  // piece), so the bank-conflict swizzle sits on the SOURCE: LDS chunk c' of row r holds channel chunk
-  // c' ^ ((r >> 2) & 3), and the fragment reads apply the same XOR (16 lanes, rows r0..r0+15, one chunk:
-  // 16 distinct 16-B slots of the 256-B bank row).
+  // Operand tiles are copied global -> LDS by LDS-DMA (no register staging). The DMA writes lane-linearly
+  // (16 rows x 64 B per piece), so the bank-conflict swizzle sits on the SOURCE: LDS chunk c' of row r holds
+  // channel chunk c' ^ ((r >> 2) & 3), and the fragment reads apply the same XOR (16 lanes reading 16
+  // consecutive rows, one chunk: 16 distinct 16-B slots of the 256-B bank row, at any starting row).
+  //  HALO = false: K steps in (tap, 32-channel) order; each step's A tile [BM co][32 ci] and B tile
+  //   [BN t][32 ci] go into an NS-deep ring, step st + NS - 1 issued while step st's MFMAs run, a counted
+  //   vmcnt waits for the wave's own pieces of step st.
+  //  HALO = true: K steps in (32-channel, tap) order; per channel step the activation rows of ALL taps
+  //   (BN + (taps - 1) |tap_step| rows, the halo) are copied once into one of two halo buffers and each
+  //   tap reads its fragments at its row offset, so a step streams only its A tile (8 KB at BM = 128,
+  //   against 16 KB with the B tile): the next channel step's halo is issued at this one's first tap.
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int NPA = BM / 16, NP = (BM + BN) / 16;  // 1 KiB pieces per step
-  constexpr int STAGE = (BM + BN) * 64, TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
-  constexpr int LDS_BYTES = NS * STAGE > TILE_BYTES ? NS * STAGE : TILE_BYTES;
+  constexpr int STAGE = HALO ? BM * 64 : (BM + BN) * 64, NSA = HALO ? 2 : NS;
+  constexpr int HBUF = HALO ? HALO_PIECES * 1024 : 0;
+  constexpr int TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
+  constexpr int RING = NSA * STAGE + 2 * HBUF;
+  constexpr int LDS_BYTES = RING > TILE_BYTES ? RING : TILE_BYTES;
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];
   float(&tile)[BN / 2][TP] = *reinterpret_cast<float(*)[BN / 2][TP]>(lds_raw);
   const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
@@ -103,54 +112,105 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   const int in_off = a.nphase > 1 ? (rho + a.phase_pad) / a.out_stride : a.in_off;
   const int out_phase = a.nphase > 1 ? rho : a.out_phase;
   const int nci = a.c_in / 32, nsteps = a.taps * nci;
-  const int npw = (NP - wave + 3) / 4;  // this wave's pieces per step: p = wave, wave + 4, ...
   // per-lane piece geometry: row 16 p + (lane >> 2), LDS chunk lane & 3, source chunk swizzled
   const int prow = lane >> 2, pchunk = (lane & 3) ^ ((lane >> 4) & 3);
-  auto issue = [&](int st_) {
-    const int tap_ = st_ / nci, ci_ = (st_ - tap_ * nci) * 32 + pchunk * 8;
-    char* stg = lds_raw + (st_ % NS) * STAGE;
-#pragma unroll
-    for (int k = 0; k < (NP + 3) / 4; ++k) {
-      const int p = wave + 4 * k;
-      if (p < NP) {
-        const void* src;
-        if (p < NPA) {
-          src = wts + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_;
-        } else {
-          const int q = q_blk + 16 * (p - NPA) + prow;
-          const int tin = q + in_off + tap_ * a.tap_step;
-          const bool ok = q < a.n_out && tin >= 0 && tin < a.t_in;
-          src = ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3];
-        }
-        glds16(src, stg + p * 1024);
-      }
-    }
-  };
   const int am = wm * (16 * WM), bn = wn * (16 * WN);
-  const int rslot = ((lane >> 4) ^ ((lr >> 2) & 3)) * 16;  // swizzled byte offset of this lane's fragment
-#pragma unroll
-  for (int k = 0; k < NS - 1; ++k)
-    if (k < nsteps) issue(k);
-  for (int st = 0; st < nsteps; ++st) {
-    // outstanding after step st's pieces: those of steps st + 1 .. st + NS - 2 that were issued
-    wait_vm(npw * (min(nsteps - 1, st + NS - 2) - st));
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (st + NS - 1 < nsteps) issue(st + NS - 1);
-    const char* stg = lds_raw + (st % NS) * STAGE;
+  const int rslot = ((lane >> 4) ^ ((lr >> 2) & 3)) * 16;  // swizzled byte offset of this lane's A fragment
+  auto mfma_step = [&](const char* as, const char* bs, int boff) {
     uint4 af[WM], bfr[WN];
 #pragma unroll
-    for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const uint4*>(stg + (am + i * 16 + lr) * 64 + rslot);
+    for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const uint4*>(as + (am + i * 16 + lr) * 64 + rslot);
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
-      bfr[j] = *reinterpret_cast<const uint4*>(stg + BM * 64 + (bn + j * 16 + lr) * 64 + rslot);
+    for (int j = 0; j < WN; ++j) {
+      const int r = bn + j * 16 + lr + boff;
+      bfr[j] = *reinterpret_cast<const uint4*>(bs + r * 64 + (((lane >> 4) ^ ((r >> 2) & 3)) * 16));
+    }
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
       for (int j = 0; j < WN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, af[i]),
                                                            __builtin_bit_cast(f16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
-    asm volatile("" ::: "memory");
+  };
+  if constexpr (HALO) {
+    const int span = (a.taps - 1) * abs(a.tap_step);
+    const int omin = in_off + min(0, (a.taps - 1) * a.tap_step);  // first input row of the halo, from q_blk
+    const int nbp = (BN + span + 15) / 16;                        // halo pieces (host-checked <= HALO_PIECES)
+    char* const abuf = lds_raw;
+    char* const hbuf = lds_raw + 2 * STAGE;
+    auto issue_a = [&](int st_) {
+      const int cs = st_ / a.taps, tap_ = st_ - cs * a.taps;
+      const int ci_ = cs * 32 + pchunk * 8;
+#pragma unroll
+      for (int k = 0; k < (NPA + 3) / 4; ++k) {
+        const int p = wave + 4 * k;
+        if (p < NPA)
+          glds16(wts + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_,
+                 abuf + (st_ & 1) * STAGE + p * 1024);
+      }
+    };
+    auto issue_halo = [&](int cs) {
+      const int ci_ = cs * 32 + pchunk * 8;
+      for (int p = wave; p < nbp; p += 4) {
+        const int tin = q_blk + omin + 16 * p + prow;
+        const bool ok = tin >= 0 && tin < a.t_in;
+        glds16(ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3],
+               hbuf + (cs & 1) * HBUF + p * 1024);
+      }
+    };
+    issue_halo(0);
+    issue_a(0);
+    int cs = 0, tap = 0;
+    for (int st = 0; st < nsteps; ++st) {
+      wait_vm(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // after the barrier every wave is done with step st - 1: its A buffer and (at tap 0) the halo
+      // buffer of channel step cs - 1 are free
+      if (st + 1 < nsteps) issue_a(st + 1);
+      if (tap == 0 && cs + 1 < nci) issue_halo(cs + 1);
+      mfma_step(abuf + (st & 1) * STAGE, hbuf + (cs & 1) * HBUF, in_off + tap * a.tap_step - omin);
+      asm volatile("" ::: "memory");
+      if (++tap == a.taps) {
+        tap = 0;
+        ++cs;
+      }
+    }
+  } else {
+    const int npw = (NP - wave + 3) / 4;  // this wave's pieces per step: p = wave, wave + 4, ...
+    auto issue = [&](int st_) {
+      const int tap_ = st_ / nci, ci_ = (st_ - tap_ * nci) * 32 + pchunk * 8;
+      char* stg = lds_raw + (st_ % NS) * STAGE;
+#pragma unroll
+      for (int k = 0; k < (NP + 3) / 4; ++k) {
+        const int p = wave + 4 * k;
+        if (p < NP) {
+          const void* src;
+          if (p < NPA) {
+            src = wts + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_;
+          } else {
+            const int q = q_blk + 16 * (p - NPA) + prow;
+            const int tin = q + in_off + tap_ * a.tap_step;
+            const bool ok = q < a.n_out && tin >= 0 && tin < a.t_in;
+            src = ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3];
+          }
+          glds16(src, stg + p * 1024);
+        }
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+      if (k < nsteps) issue(k);
+    for (int st = 0; st < nsteps; ++st) {
+      // outstanding after step st's pieces: those of steps st + 1 .. st + NS - 2 that were issued
+      wait_vm(npw * (min(nsteps - 1, st + NS - 2) - st));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (st + NS - 1 < nsteps) issue(st + NS - 1);
+      const char* stg = lds_raw + (st % NS) * STAGE;
+      mfma_step(stg, stg + BM * 64, 0);
+      asm volatile("" ::: "memory");
+    }
   }
   __syncthreads();  // every wave's last fragment reads are done before the ring is reused as the output tile
   const int tid = threadIdx.x;
@@ -408,7 +468,15 @@ static int launch_conv(const ConvArgs& a, hipStream_t s) {
   const dim3 grid(nq, (unsigned)(a.c_out / (32 * wm)), nz);
   // ring depth 2: measured against 3 and 4 (3.60 / 3.74 / 4.14 ms DAC decode at 861 frames): the deeper
   // rings' LDS costs more than their extra step of load lookahead gains
-#define ZMI_CONV_L(wm_) hipLaunchKernelGGL((conv_kernel<wm_, WN, 2>), grid, dim3(256), 0, s, a)
+  const int span = (a.taps - 1) * abs(a.tap_step);
+  // the halo K order wherever the taps' rows fit its buffer (every DAC conv: dilation <= 9, span <= 54);
+  // measured 3.7 -> 3.15 ms DAC decode, 2.11 -> 1.83 ms encode at 861 frames against the tap-major order
+  const bool halo = BN + span <= HALO_PIECES * 16;
+#define ZMI_CONV_L(wm_)                                                                     \
+  do {                                                                                      \
+    if (halo) hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, true>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, false>), grid, dim3(256), 0, s, a);     \
+  } while (0)
   switch (wm) {
     case 4: ZMI_CONV_L(4); break;
     case 3: ZMI_CONV_L(3); break;
