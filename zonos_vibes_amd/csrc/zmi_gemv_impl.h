@@ -174,18 +174,21 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
 
   // (1) activation rows (+ LayerNorm gamma / beta, first tile only) into LDS by DMA, 1 KiB pieces
   // spread over waves; then the tile's epilogue operands
-  auto stage = [&](bool first) {
+  // the DMA of a tile's rows (s_row0, s_rows, s_X) is split from its epilogue operands: in the multi-tile
+  // loop the next tile's rows are issued as soon as every wave's MFMA chain has left the LDS image, under
+  // the current tile's reduction and epilogue
+  auto stage_rows = [&](bool first, int s_row0, int s_rows, const bf16_t* s_X) {
     constexpr int PPR = K / 512;
-    const int n_x = rows * PPR;
+    const int n_x = s_rows * PPR;
     constexpr int APR = PRO == PRO_GRMS ? 2 * PPR : PPR;  // aux pieces per row (f32 gate rows: twice the bytes)
-    const int n_a = AUX ? rows * APR : 0;
+    const int n_a = AUX ? s_rows * APR : 0;
     const int n_pc = n_x + n_a + (first ? GB * PPR : 0);
-    const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)row0 * a.ld_aux * (PRO == PRO_GRMS ? 2 : 1)
+    const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)s_row0 * a.ld_aux * (PRO == PRO_GRMS ? 2 : 1)
                            : nullptr;
     for (int pc = wave; pc < n_pc; pc += NWV) {
       if (pc < n_x) {
         const int r = pc / PPR, p = pc - r * PPR;
-        dma_piece(X + (size_t)r * a.ldx + p * 512 + lane * 8, xs + r * XROW + p * 512);
+        dma_piece(s_X + (size_t)r * a.ldx + p * 512 + lane * 8, xs + r * XROW + p * 512);
       } else if (pc < n_x + n_a) {
         const int r = (pc - n_x) / APR, p = (pc - n_x) - r * APR;
         if (PRO == PRO_GRMS)  // 1 KiB = 256 f32 of the gate row
@@ -199,6 +202,8 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
         dma_piece(src + p * 512 + lane * 8, (which ? bet : gam) + p * 512);
       }
     }
+  };
+  auto stage_epi = [&]() {
 #pragma unroll
     for (int i = 0; i < NE; ++i) res_pre[i] = 0;
     q_pos = -1;
@@ -216,7 +221,8 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
       q_kvr = a.row_kv[row0 + (lane >> 2)];
     }
   };
-  stage(true);
+  stage_rows(true, row0, rows, X);
+  stage_epi();
   __builtin_amdgcn_sched_barrier(0);
   // (2) the whole weight slice of this lane, in flight at once: one buffer descriptor per wave
   // (wave-uniform base), lane offset in the VGPR, chunk offset j KiB folded into the instruction
@@ -421,6 +427,10 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   }
   __syncthreads();
   ZMI_GSTAMP(5);
+  if (!NTW && rt + 1 < rt_end) {  // every chain is done with the LDS image: the next tile's rows go in now
+    const int n_row0 = (rt + 1) * RT;
+    stage_rows(false, n_row0, min(RT, a.M - n_row0), reinterpret_cast<const bf16_t*>(a.X) + (size_t)n_row0 * a.ldx);
+  }
   if (ew) {
   auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
     float v = red[((gi * W) * 8 + c) * RT + r];
@@ -526,7 +536,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   row0 = rt * RT;
   rows = min(RT, a.M - row0);
   X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)row0 * a.ldx;
-  stage(false);
+  stage_epi();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's rows (the weights landed long ago)
   }  // row tiles
 }
