@@ -551,7 +551,9 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
 // slice as few times as that allows (speed only: a row's arithmetic does not depend on it)
 inline int rows_per_wg(int n_cb, int n_rt) {
   if (n_rt <= 1) return 1;
-  const int n_rg = std::max(1, std::min(n_rt, 1024 / std::max(1, n_cb)));
+  // ~512 workgroups: fewer row groups re-read each weight slice (C3 sample 102 -> 104x against ~1024;
+  // 256 and 2048 were slower, the prefill did not move)
+  const int n_rg = std::max(1, std::min(n_rt, 512 / std::max(1, n_cb)));
   return (n_rt + n_rg - 1) / n_rg;
 }
 
