@@ -549,11 +549,12 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
 
 // row tiles per workgroup: enough workgroups to fill the chip (~4 per CU), each re-reading its weight
 // slice as few times as that allows (speed only: a row's arithmetic does not depend on it)
-inline int rows_per_wg(int n_cb, int n_rt) {
+inline int rows_per_wg(int n_cb, int n_rt, int target) {
   if (n_rt <= 1) return 1;
-  // ~512 workgroups: fewer row groups re-read each weight slice (C3 sample 102 -> 104x against ~1024;
-  // 256 and 2048 were slower, the prefill did not move)
-  const int n_rg = std::max(1, std::min(n_rt, 512 / std::max(1, n_cb)));
+  // about `target` workgroups: fewer row groups re-read each weight slice. Measured on the C3 sample:
+  // 512 (K = 2048) against ~1024: 102 -> 104x, 256 and 2048 slower, the prefill unmoved; 256 for the
+  // K = 8192 fc2 (1024-thread workgroups, 256 KB weight slices): 9,740 -> 9,960 frames/s, 128 slower
+  const int n_rg = std::max(1, std::min(n_rt, target / std::max(1, n_cb)));
   return (n_rt + n_rg - 1) / n_rg;
 }
 
@@ -605,7 +606,7 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
                             (int)LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
-  const int rpw = rows_per_wg(n_cb, n_rt);
+  const int rpw = rows_per_wg(n_cb, n_rt, K == 8192 ? 256 : 512);
   const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * ((n_rt + rpw - 1) / rpw);
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt, rpw);
