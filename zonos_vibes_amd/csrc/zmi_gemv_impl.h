@@ -584,12 +584,13 @@ inline int groups_for(const ZmiGemvArgs& a, const Shape& s) {
   if (a.groups > 0) return a.groups;
   // two groups also for plain rows when there are many of them: each workgroup's activation tiles
   // then serve 16 columns (a 128-row fc1 re-read its rows from L2 per 8-column group: ~1 GB a launch)
-  if (a.K == 8192 && a.M > 16 && a.N / 8 >= 256) return 2;  // fc2 over many rows: 16 KB activation rows
+  // (from 5 rows: the pre-normalised plans; C5's 16-row step 2.03 -> 1.87 ms with both K = 2048 and 8192 at 2)
+  if (a.K == 8192 && a.M > 4 && a.N / 8 >= 256) return 2;  // fc2 over many rows: 16 KB activation rows
   // 4 groups (1024 threads) for the plain K = 2048 GEMVs over many rows (qkv, out_proj, fc1, heads of the
   // multi-slot decode and the prefill): each staged activation tile serves 32 columns, halving the tile
   // re-reads of 2 groups (C3 sample 9,050 -> 9,710 frames/s)
   if (a.K == 2048 && a.M > 16 && a.N / 8 >= 256 && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO) return 4;
-  return (a.K == 2048 && a.N / 8 >= 384 && (a.ln_w != nullptr || a.pro != ZMI_PRO_AUTO || a.M > 16)) ? 2 : 1;
+  return (a.K == 2048 && a.N / 8 >= 384 && (a.ln_w != nullptr || a.pro != ZMI_PRO_AUTO || a.M > 4)) ? 2 : 1;
 }
 
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>

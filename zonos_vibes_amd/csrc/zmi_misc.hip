@@ -83,16 +83,23 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const bf16_t* x, in
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= m) return;
   const bf16_t* xr = x + (size_t)r * ldx;
-  uint4 xv[NQ][CPQ];
+  uint4 xv[NQ][CPQ], gw[NQ][CPQ], gb[NQ][CPQ];
   float p[NQ];
+  // the row, gamma and beta loads all in flight together (one memory round trip, not two)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int i = 0; i < CPQ; ++i) {
+      const int c = q * (K / NQ) / 8 + lane + 64 * i;
+      xv[q][i] = *reinterpret_cast<const uint4*>(xr + q * (K / NQ) + (lane + 64 * i) * 8);
+      gw[q][i] = reinterpret_cast<const uint4*>(w)[c];
+      gb[q][i] = reinterpret_cast<const uint4*>(b)[c];
+    }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < CPQ; ++i) {
-      xv[q][i] = *reinterpret_cast<const uint4*>(xr + q * (K / NQ) + (lane + 64 * i) * 8);
-      t += ln_chunk_sum(xv[q][i], 0.f, false);
-    }
+    for (int i = 0; i < CPQ; ++i) t += ln_chunk_sum(xv[q][i], 0.f, false);
     p[q] = wave_sum(t);
   }
   const float mean = ln_combine<NQ>(p) / (float)K;
@@ -109,8 +116,7 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const bf16_t* x, in
 #pragma unroll
     for (int i = 0; i < CPQ; ++i) {
       const int c = q * (K / NQ) / 8 + lane + 64 * i;
-      const uint4 gw = reinterpret_cast<const uint4*>(w)[c], gb = reinterpret_cast<const uint4*>(b)[c];
-      reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = ln_apply(xv[q][i], gw, gb, rstd, nbias);
+      reinterpret_cast<uint4*>(out + (size_t)r * ldo)[c] = ln_apply(xv[q][i], gw[q][i], gb[q][i], rstd, nbias);
     }
 }
 }  // namespace
