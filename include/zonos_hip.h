@@ -108,7 +108,9 @@ int zmi_attention_max_keys_whole(void);
  * hand-off granules; a row's words must not hold tag pos + 1 from an earlier use when it runs at
  * position pos (zero them when a row starts a new utterance; consecutive steps need nothing).
  * err: set nonzero if a wait gave up. slices: 4 or 8 workgroups per (row, kv head).
- * Positions < zmi_attention_max_keys_whole(). */
+ * Positions < zmi_attention_max_keys_whole(). The projection's prologue is LayerNorm (pro AUTO with ln_w) or
+ * ADDLN (pro ZMI_PRO_ADDLN: the hybrid's layer_norm_fn(hidden, residual), aux / ld_aux / res_out as for
+ * zmi_gemv_launch). */
 int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                    void* stream);
 int64_t zmi_attn_block_gran_words(int rows, int hkv);
