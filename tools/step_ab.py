@@ -23,6 +23,9 @@ OPTIONS = [dict(prefetch_blocks=0), dict(prefetch_blocks=192, prefetch_fc1_mb=0)
 
 
 def main():
+    global OPTIONS
+    if len(sys.argv) > 1:  # a JSON list of option dicts replaces the default set
+        OPTIONS = json.loads(sys.argv[1])
     dev = torch.device("cuda", 0)
     cfg = zonos_v01_transformer()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=bench.LC + bench.N_NEW + 9,

@@ -104,6 +104,7 @@ class HipEngine:
         # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only)
         self.prefetch_blocks = 192
         self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
+        self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
         self._plans: dict[int, list] = {}
         self._graphs: dict[int, int] = {}
         self.n_kv = self._kv_layers()
@@ -291,8 +292,10 @@ class HipEngine:
                                                 self.F, ln=ln)))
                 plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
             xin, ln = normed((w["nf_w"], w["nf_b"]))
-            plan.append(("gemv", self._gemv(w["heads"], xin, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
-                                            n_valid=HEADS_N, ln=ln)))
+            heads = self._gemv(w["heads"], xin, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
+                               n_valid=HEADS_N, ln=ln)
+            heads[0].groups = self.heads_groups
+            plan.append(("gemv", heads))
             self._plans[rows] = plan
         return self._plans[rows]
 
