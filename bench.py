@@ -72,7 +72,7 @@ def pmc_traffic():
     rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950 correction; a counter pass
     serialises dispatches, so it is not repeated inside the timed run). None when the profile is
     absent or measured another kernel."""
-    path = os.path.join(REPO, "profiles", "r02f_pmc_fc1_fetch.json")
+    path = os.path.join(REPO, "profiles", "r02g_pmc_fc1_fetch.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -502,7 +502,7 @@ def main():
             "roofline": {"kernel": "gemv_kernel<G=2,W=4,NL=8,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
-                         "traffic_source": "profiles/r02f_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "traffic_source": "profiles/r02g_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "utterance_breakdown": breakdown,
             "widened": widened,
