@@ -287,6 +287,10 @@ int zmi_gated_rmsnorm(const void* y, int ldy, const void* z, int ldz, int m, int
  * separate launches; *err becomes nonzero if a wait timed out. */
 int zmi_mamba_block(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err, void* stream);
 int64_t zmi_mamba_block_gran_words(int rows, int d_in_proj);
+/* zmi_mamba_block plus `prefetch->blocks` prefetch-only workgroups (ZmiPrefetch, as zmi_attn_block_pf) that
+ * read the given ranges (the layer's out_proj weights) once during the step phase; same results. */
+int zmi_mamba_block_pf(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err,
+                       const ZmiPrefetch* prefetch, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Synthetic weights: fill with the counter-based uniform stream of zonos_vibes_amd/synthetic.py

@@ -21,9 +21,12 @@ def main():
     cfg = zonos_v01_hybrid()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n + 9, max_prefill=LC + 1)
     cond = cond_tensor(1, cfg.backbone.d_model, dev)
-    res = {True: [], False: []}
+    # "name" toggles a bool; "name=v1,v2" alternates integer values
+    vals = [int(v) for v in flag.split("=")[1].split(",")] if "=" in flag else [True, False]
+    flag = flag.split("=")[0]
+    res = {v: [] for v in vals}
     for rep in range(3):
-        for on in (True, False):
+        for on in vals:
             setattr(m.engine, flag, on)
             m.engine._build_plan()
             m.generate(cond, max_new_tokens=n, sampling_params=dict(temperature=0.0), progress_bar=False, chunk=128)
@@ -34,7 +37,7 @@ def main():
             torch.cuda.synchronize()
             res[on].append(round((time.perf_counter() - t0) * 1e3, 1))
             assert codes.shape[-1] == n
-    print(json.dumps({"flag": flag, "frames": n, "generate_ms_on": res[True], "generate_ms_off": res[False]}))
+    print(json.dumps({"flag": flag, "frames": n, "generate_ms": {str(k): v for k, v in res.items()}}))
 
 
 if __name__ == "__main__":

@@ -123,6 +123,8 @@ _SIGS = {
     "zmi_add_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                   c_void_p, c_int, c_int, c_void_p]),
     "zmi_mamba_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(Mamba2Args), c_void_p, c_void_p, c_void_p]),
+    "zmi_mamba_block_pf": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(Mamba2Args), c_void_p, c_void_p,
+                                   ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_mamba_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_gated_rmsnorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_int,
                                   c_void_p]),

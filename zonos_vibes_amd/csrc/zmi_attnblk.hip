@@ -27,6 +27,7 @@
 #include "zmi_common.h"
 #include "zmi_kernels.h"
 #include "zmi_gemv_impl.h"
+#include "zmi_prefetch.h"
 #include "zmi_attn_ds.h"
 
 namespace {
@@ -436,32 +437,6 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   ZMI_ASTAMP(6);
 }
 
-// Prefetch role (optional): while the attention runs, HBM is nearly idle for several microseconds; these
-// workgroups (dispatched on the CUs the projection vacates) read the next launches' weights (out_proj,
-// the head of fc1) once with default-policy loads, so those launches find them in the Infinity Cache.
-// Nothing waits on them and nothing they read is written in this launch.
-__device__ __forceinline__ void prefetch_body(const ZmiPrefetch& pf, int j, int n_pf) {
-  unsigned acc = 0;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const uint4* p = reinterpret_cast<const uint4*>(pf.ptr[r]);
-    const int64_t nvec = pf.bytes[r] / 16;
-    const int64_t per = (nvec + n_pf - 1) / n_pf;
-    const int64_t lo = (int64_t)j * per, hi = min(lo + per, nvec);
-    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * NT) {
-      uint4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t i = i0 + (int64_t)u * NT;
-        v[u] = i < hi ? p[i] : uint4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    }
-  }
-  if (acc == 0x9E3779B9u && pf.sink) *pf.sink = acc;  // keeps the loads; the sink is never read
-}
-
 // PRO: the projection's prologue, LayerNorm (transformer blocks) or ADDLN (the hybrid's MHA blocks:
 // layer_norm_fn(hidden, residual) with the new residual written by column block 0)
 template <int S, int PRO>
@@ -476,7 +451,7 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
   else if (b < n_qkv + n_xs)
     xs_body<S>(at, n_units, b - n_qkv, smem, gran);
   else
-    prefetch_body(pf, b - n_qkv - n_xs, n_pf);
+    prefetch_body<NT>(pf, b - n_qkv - n_xs, n_pf);
 }
 
 template <int S, int PRO>
@@ -545,9 +520,7 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   ZmiPrefetch pf{};
   if (prefetch) {
     pf = *prefetch;
-    if (pf.bytes[0] < 0 || pf.bytes[1] < 0 || (pf.bytes[0] && !pf.ptr[0]) || (pf.bytes[1] && !pf.ptr[1]) ||
-        pf.blocks < 0 || pf.blocks > 4096 || ((pf.bytes[0] | pf.bytes[1]) && pf.blocks == 0))
-      return zmi_fail_msg("attn_block: bad prefetch ranges");
+    if (zmi_prefetch_invalid(pf)) return zmi_fail_msg("attn_block: bad prefetch ranges");
   }
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;

@@ -21,6 +21,7 @@
 #include "zmi_kernels.h"
 #include "zmi_gemv_impl.h"
 #include "zmi_mamba_step.h"
+#include "zmi_prefetch.h"
 
 namespace {
 
@@ -32,12 +33,17 @@ constexpr unsigned SPIN = 1u << 20;
 
 __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, int n_cb, int n_in,
                                                          const ZmiMamba2Args ma, uint64_t* gran, int gstride,
-                                                         unsigned* err) {
+                                                         unsigned* err, const ZmiPrefetch pf, int n_pf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   if (b < n_in) {
     zmi_gemv::gemv_body<IG, IW, INL, IRT, zmi_gemv::PRO_ADDLN, ZMI_EPI_STORE, 1, 2>(
         ia, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, gstride});
+    return;
+  }
+  const int n_step = ma.M * ma.nheads;
+  if (b >= n_in + n_step) {  // prefetch role: the out_proj weights, under the step's latency chain
+    prefetch_body<NT>(pf, b - n_in - n_step, n_pf);
     return;
   }
   const int b2 = b - n_in;
@@ -106,8 +112,8 @@ extern "C" int64_t zmi_mamba_block_gran_words(int rows, int d_in_proj) {
   return (rows <= 0 || d_in_proj <= 0 || d_in_proj % 2) ? -1 : (int64_t)rows * (d_in_proj / 2);
 }
 
-extern "C" int zmi_mamba_block(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err,
-                               void* stream) {
+extern "C" int zmi_mamba_block_pf(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err,
+                                  const ZmiPrefetch* prefetch, void* stream) {
   const ZmiGemvArgs& a = *in_proj;
   const ZmiMamba2Args& s = *step;
   if (a.K != 2048 || a.pro != ZMI_PRO_ADDLN || !a.ln_w || !a.ln_b || !a.aux || a.ld_aux % 8 || a.res_out == a.aux)
@@ -133,8 +139,19 @@ extern "C" int zmi_mamba_block(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* 
                                                        (int)zmi_gemv::LDS_MAX);
     if (attr != hipSuccess) return zmi_fail(attr, "hipFuncSetAttribute", __FILE__, __LINE__);
   }
-  hipLaunchKernelGGL(mamba_block_kernel, dim3((unsigned)(n_in + a.M * s.nheads)), dim3(NT), lds, (hipStream_t)stream,
-                     a, n_cb, n_in, s, (uint64_t*)gran, a.N / 2, err);
+  ZmiPrefetch pf{};
+  if (prefetch) {
+    pf = *prefetch;
+    if (zmi_prefetch_invalid(pf)) return zmi_fail_msg("mamba_block: bad prefetch ranges");
+  }
+  const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
+  hipLaunchKernelGGL(mamba_block_kernel, dim3((unsigned)(n_in + a.M * s.nheads + n_pf)), dim3(NT), lds,
+                     (hipStream_t)stream, a, n_cb, n_in, s, (uint64_t*)gran, a.N / 2, err, pf, n_pf);
   ZMI_CHECK(hipGetLastError());
   return 0;
+}
+
+extern "C" int zmi_mamba_block(const ZmiGemvArgs* in_proj, const ZmiMamba2Args* step, void* gran, unsigned* err,
+                               void* stream) {
+  return zmi_mamba_block_pf(in_proj, step, gran, err, nullptr, stream);
 }

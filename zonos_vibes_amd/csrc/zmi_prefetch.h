@@ -1,0 +1,37 @@
+// Prefetch-only workgroup role shared by the fused launches (zmi_attn_block, zmi_mamba_block): while a
+// launch's latency-bound phase runs (attention, the Mamba2 step) HBM is nearly idle for several
+// microseconds; these workgroups (dispatched last, on the CUs the projection vacates) read the next
+// launch's weights once with default-policy loads, so that launch finds them in the Infinity Cache.
+// Nothing waits on them and nothing they read is written in the launch.
+#pragma once
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+
+template <int NTH>
+__device__ __forceinline__ void prefetch_body(const ZmiPrefetch& pf, int j, int n_pf) {
+  unsigned acc = 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const uint4* p = reinterpret_cast<const uint4*>(pf.ptr[r]);
+    const int64_t nvec = pf.bytes[r] / 16;
+    const int64_t per = (nvec + n_pf - 1) / n_pf;
+    const int64_t lo = (int64_t)j * per, hi = min(lo + per, nvec);
+    for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * NTH) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t i = i0 + (int64_t)u * NTH;
+        v[u] = i < hi ? p[i] : uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  if (acc == 0x9E3779B9u && pf.sink) *pf.sink = acc;  // keeps the loads; the sink is never read
+}
+
+// host-side check of a prefetch request: 0 if valid
+inline int zmi_prefetch_invalid(const ZmiPrefetch& pf) {
+  return pf.bytes[0] < 0 || pf.bytes[1] < 0 || (pf.bytes[0] && !pf.ptr[0]) || (pf.bytes[1] && !pf.ptr[1]) ||
+         pf.blocks < 0 || pf.blocks > 4096 || ((pf.bytes[0] | pf.bytes[1]) && pf.blocks == 0);
+}

@@ -65,6 +65,9 @@ class HybridEngine(HipEngine):
         self.attn_block = True
         # decode in_proj + Mamba2 step as ONE launch (zmi_mamba_block) for <= 16 rows at d_model 2048
         self.mamba_block = True
+        # prefetch the layer's out_proj weights into the Infinity Cache during the step phase: measured slower
+        # (C4 300 frames: 320 ms off; 321, 333 and 361 ms with 64, 192 and 32 prefetch workgroups), so off
+        self.mamba_prefetch = False
 
     def _kv_layers(self) -> int:
         return len(self.attn_idx)
@@ -180,12 +183,17 @@ class HybridEngine(HipEngine):
                                              md["d_ssm"], s), "gated_rmsnorm")
         return run
 
-    def _call_mamba_block(self, ia, sa, gran):
+    def _call_mamba_block(self, ia, sa, gran, out_w=None):
         lib, s, ep, gp = self.lib, self.sptr, self.blk_err.data_ptr(), gran.data_ptr()
         ia.row_pos = sa.row_pos  # the in_proj epilogue tags its granules with the row's position + 1
+        pf = _lib.Prefetch()
+        if out_w is not None and self.prefetch_blocks > 0:  # out_proj's weights into the Infinity Cache
+            pf.ptr[0], pf.bytes[0] = out_w.data_ptr(), out_w.numel() * 2
+            pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
 
         def run():
-            _lib.check(lib.zmi_mamba_block(ctypes.byref(ia), ctypes.byref(sa), gp, ep, s), "mamba_block")
+            _lib.check(lib.zmi_mamba_block_pf(ctypes.byref(ia), ctypes.byref(sa), gp, ep, ctypes.byref(pf), s),
+                       "mamba_block")
         return run
 
     def _call_step(self, a):
@@ -284,7 +292,8 @@ class HybridEngine(HipEngine):
                     if fuse_g:
                         sa.gz = self.gz.data_ptr()
                     if self.mamba_block and d == 2048 and rows <= 16:
-                        plan.append(("call", self._call_mamba_block(inp[1][0], sa, self.mgran[lw["st"]])))
+                        plan.append(("call", self._call_mamba_block(inp[1][0], sa, self.mgran[lw["st"]],
+                                                                    lw["out"] if self.mamba_prefetch else None)))
                     else:
                         plan.append(inp)
                         plan.append(("call", self._call_step(sa)))
