@@ -107,12 +107,20 @@ int zmi_attention_max_keys_whole(void);
  * zmi_attention. gran: zmi_attn_block_gran_words(M, hkv) u64 words of {value, tag = position + 1}
  * hand-off granules; a row's words must not hold tag pos + 1 from an earlier use when it runs at
  * position pos (zero them when a row starts a new utterance; consecutive steps need nothing).
- * err: set nonzero if a wait gave up. slices: 4 or 8 workgroups per (row, kv head).
- * Positions < zmi_attention_max_keys_whole(). The projection's prologue is LayerNorm (pro AUTO with ln_w) or
+ * err: set nonzero if a wait gave up (or a row's position exceeds the form's reach, see below).
+ * slices: 4 or 8 workgroups per (row, kv head), optionally | ZMI_ATTNBLK_SELF:
+ *   plain      the slices exchange scores (each scores 1/slices of the keys); positions < 1280;
+ *   SELF       every slice scores all keys itself, nothing is exchanged between slices; positions < 1024;
+ *   SPLIT      (slices 8) one workgroup per 128-key chunk: each reads only its chunk's K / V, the chunks
+ *              exchange their maxima and P.V partials (two small hand-offs); positions < 1024.
+ * zmi_attn_block_max_pos(slices) is the last position the form accepts; any smax is allowed (the engine
+ * picks the form per step from the rows' positions). The projection's prologue is LayerNorm (pro AUTO with ln_w) or
  * ADDLN (pro ZMI_PRO_ADDLN: the hybrid's layer_norm_fn(hidden, residual), aux / ld_aux / res_out as for
  * zmi_gemv_launch). */
 int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                    void* stream);
+enum { ZMI_ATTNBLK_SELF = 256, ZMI_ATTNBLK_SPLIT = 512 };
+int zmi_attn_block_max_pos(int slices);
 int64_t zmi_attn_block_gran_words(int rows, int hkv);
 /* zmi_attn_block plus `blocks` prefetch-only workgroups that read ptr[0..1][0 .. bytes) once during the
  * attention phase (HBM is nearly idle there): the next launches' weights (out_proj, the head of fc1) are

@@ -82,15 +82,22 @@ def _fused(st, slices, reps=1):
     return q, kc, vt, out
 
 
+SELF, SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms (positions < 1024)
+
+
 @pytest.mark.parametrize("positions", [
     (591, 592),                                    # C2 mean position, one slot
     (0, 1),                                        # the first key comes from this launch only
     (127, 128, 511, 512, 1030, 1279),              # chunk / block edges and the last covered position
     (5, -1, 300, 301, 63, 64, 700, -1, 1000, 1001, 31, 32, 255, 256, 900, 17),  # 16 rows, inactive rows
 ])
-@pytest.mark.parametrize("slices", [4, 8])
-def test_attn_block_bit_identical_to_separate_launches(positions, slices):
-    st = _setup(positions, 1280, seed=70)
+@pytest.mark.parametrize("slices", [4, 8, 4 | SELF, 8 | SELF, 8 | SPLIT])
+@pytest.mark.parametrize("smax", [1280, 2056])
+def test_attn_block_bit_identical_to_separate_launches(positions, slices, smax):
+    if slices & (SELF | SPLIT):  # these forms reach position 1023: keep the edges inside it
+        positions = tuple(p if p < 1024 else p - 256 for p in positions) + ((1023,) if len(positions) < 16 else ())
+    assert max(positions) <= _lib().lib().zmi_attn_block_max_pos(slices)
+    st = _setup(positions, smax, seed=70)
     ref = _separate(st)
     got = _fused(st, slices, reps=3)
     live = [i for i, p in enumerate(positions) if p >= 0]
@@ -101,3 +108,21 @@ def test_attn_block_bit_identical_to_separate_launches(positions, slices):
     pick = live[:3]
     _check_attention(got[3][pick], got[0][pick], got[1][pick], got[2][pick].transpose(-1, -2).contiguous(),
                      [positions[i] for i in pick])
+
+
+@pytest.mark.parametrize("slices", [8, 8 | SELF, 8 | SPLIT])
+def test_attn_block_refuses_positions_past_its_reach(slices):
+    """A row past the form's last position sets the error word instead of reading past its K / V reach."""
+    L = _lib()
+    last = L.lib().zmi_attn_block_max_pos(slices)
+    st = _setup((100, last + 1), 2056, seed=71)
+    q = torch.zeros(2, H * HD, dtype=torch.bfloat16, device=DEV)
+    kc, vt = st["kc"].clone(), st["vt"].clone()
+    a = _args(st, q, kc, vt)
+    gran = torch.zeros(L.lib().zmi_attn_block_gran_words(2, HKV), dtype=torch.int64, device=DEV)
+    err = torch.zeros(4, dtype=torch.int32, device=DEV)
+    out = torch.zeros(2, H * HD, dtype=torch.bfloat16, device=DEV)
+    L.check(L.lib().zmi_attn_block(ctypes.byref(a), gran.data_ptr(), err.data_ptr(), out.data_ptr(), H * HD,
+                                   slices, stream_ptr()), "attn_block")
+    torch.cuda.synchronize()
+    assert int(err[0].item()) != 0

@@ -362,7 +362,7 @@ def test_attn_block_addln_bit_identical_to_separate():
     for fused in (True, False):
         m.engine.attn_block = fused
         m.engine._build_plan()
-        assert any(it[0] == "attnblk" for it in m.engine._plan(2)) == fused
+        assert any(it[0] == "attnblk" for it in m.engine._plan(2, m.engine._segments(1, 1)[0][1])) == fused
         one = m.generate(conds[0], max_new_tokens=30, sampling_params=sp, progress_bar=False)
         many = m.generate_batch(conds, max_new_tokens=[20, 14, 30, 9, 25, 17, 12, 22], sampling_params=sp,
                                 seeds=list(range(8)), max_slots=8)

@@ -26,18 +26,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pos", type=int, default=591)
     ap.add_argument("--slices", type=int, default=8)
+    ap.add_argument("--form", default="split", help="split (chunk workgroups), self (self-scoring) or xs (score exchange)")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=1040, max_prefill=16)
     e = m.engine
-    e.attn_block_slices = args.slices
+    e.attn_block_slices = e.attn_self_slices = args.slices
     with torch.cuda.stream(e.stream):
         e.row_pos[:2] = args.pos
         e.row_kv[:2] = torch.arange(2, dtype=torch.int32, device=dev)
         e.x.normal_()
     e.stream.synchronize()
-    plan = e._plan(2)
+    plan = e._plan(2, args.form)
     blocks = [it for kd, it in plan if kd == "attnblk"]
     assert blocks, "the fused plan is not in use"
     buf = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
@@ -80,7 +81,7 @@ def main():
                     maxs[i].append(float(rel.max()))
         out[role] = dict(median_us=[round(sum(v) / len(v), 2) if v else None for v in meds],
                          max_us=[round(sum(v) / len(v), 2) if v else None for v in maxs])
-    print(json.dumps(dict(pos=args.pos, slices=args.slices, **out)), flush=True)
+    print(json.dumps(dict(pos=args.pos, slices=args.slices, form=args.form, **out)), flush=True)
 
 
 if __name__ == "__main__":

@@ -32,7 +32,8 @@ def main(which: str, reps: int = 2):
         e.kc.normal_()
         e.vc.normal_()
     e.stream.synchronize()
-    plan = e._plan(2)
+    e.pos_hi[0] = POS
+    plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
     for _ in range(reps):
         if which == "fc1":
             for kind, it in plan:

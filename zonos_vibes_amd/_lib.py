@@ -17,6 +17,7 @@ c_int, c_int64, c_float, c_void_p, c_uint64 = ctypes.c_int, ctypes.c_int64, ctyp
 c_int_p = ctypes.POINTER(ctypes.c_int)
 
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
+ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
 
@@ -91,6 +92,7 @@ _SIGS = {
                                       c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                       c_void_p]),
     "zmi_attention_max_keys_whole": (c_int, []),
+    "zmi_attn_block_max_pos": (c_int, [c_int]),
     "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -91,6 +91,10 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
   const int pos = a.pos[qi];
   if (pos < 0) return;
+  if (pos >= DS_KEYS) {  // the engine never launches this form past its capacity; refuse, don't read past it
+    if (threadIdx.x == 0) give_up(a);
+    return;
+  }
   ZMI_ASTAMP(0);
   const uint32_t tag = (uint32_t)pos + 1u;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, ww = wave - 1;
@@ -437,9 +441,638 @@ __device__ __forceinline__ void xs_body(const AttnArgs& a, int n_units, int b, c
   ZMI_ASTAMP(6);
 }
 
+// ---- self-scoring form (ZMI_ATTNBLK_SELF): no score exchange -------------------------------------
+// Each of the S workgroups of a (query, kv head) loads EVERY cached K row of its query (the S slices
+// sit on one XCD, so S - 1 of them read K from L2) and the V^T rows of its own HD / S output dims, and
+// computes all scores, the softmax statistics and P itself; only P.V and the output are split by
+// dims. The one hand-off left is projection -> attention (q and this position's K / V row). Wave w
+// owns 128-key chunk w for the whole chain (scores, chunk maximum, e / l / P, P.V); the waves meet
+// at three workgroup barriers (q staged, chunk maxima, chunk P.V). The arithmetic is xs_body's /
+// the chunked kernel's operation for operation (bit-identical).
+// Positions < XR_KEYS: wave w holds chunk w's K fragments (128 VGPRs) in registers.
+constexpr int FORM_XS = 0, FORM_SELF = 1, FORM_SPLIT = 2;  // attention roles of attn_block_kernel
+constexpr int XR_CH = DNW;              // chunks, one per wave
+constexpr int XR_KEYS = XR_CH * CH;     // 1024 keys (positions 0 .. 1023)
+constexpr int XR_POLL = DNW - 1;        // the wave that also receives the projection's granules
+
+template <int S>
+struct XrImg {
+  static constexpr int DSD = HD / S;
+  static constexpr size_t SC = 0;                                   // float [XG][XR_KEYS] scores
+  static constexpr size_t PB = SC + (size_t)XG * XR_KEYS * 4;       // bf16  [XG][XR_KEYS] P
+  static constexpr size_t OC = PB + (size_t)XG * XR_KEYS * 2;       // float [XR_CH][XG][DSD] chunk P.V
+  static constexpr size_t MJ = OC + (size_t)XR_CH * XG * DSD * 4;   // float [XR_CH][XG] chunk maxima
+  static constexpr size_t LJ = MJ + (size_t)XR_CH * XG * 4;         // float [XR_CH][XG] chunk exp sums
+  static constexpr size_t MB = LJ + (size_t)XR_CH * XG * 4;         // float [XR_CH / CPB][XG] M_j
+  static constexpr size_t QKV = MB + (size_t)(XR_CH / CPB) * XG * 4; // u32 [QKV_GRAN] q | k | v pairs of pos
+  static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
+};
+
+template <int S>
+__device__ __forceinline__ void xr_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
+  constexpr int DT = 8 / S;
+  using I = XrImg<S>;
+  constexpr int DSD = I::DSD;
+  float(&sc)[XG][XR_KEYS] = *reinterpret_cast<float(*)[XG][XR_KEYS]>(smem + I::SC);
+  bf16_t(&pb)[XG][XR_KEYS] = *reinterpret_cast<bf16_t(*)[XG][XR_KEYS]>(smem + I::PB);
+  float(&ocs)[XR_CH][XG][DSD] = *reinterpret_cast<float(*)[XR_CH][XG][DSD]>(smem + I::OC);
+  float(&mjc)[XR_CH][XG] = *reinterpret_cast<float(*)[XR_CH][XG]>(smem + I::MJ);
+  float(&ljc)[XR_CH][XG] = *reinterpret_cast<float(*)[XR_CH][XG]>(smem + I::LJ);
+  float(&mblk)[XR_CH / CPB][XG] = *reinterpret_cast<float(*)[XR_CH / CPB][XG]>(smem + I::MB);
+  uint32_t* qkv_lds = reinterpret_cast<uint32_t*>(smem + I::QKV);
+
+  const int y = b >> 3;
+  const int s = y % S, unit = 8 * (y / S) + (b & 7);
+  if (unit >= n_units) return;
+  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
+  const int pos = a.pos[qi];
+  if (pos < 0) return;
+  if (pos >= XR_KEYS) {  // the engine never launches this form past its capacity; refuse, don't read past it
+    if (threadIdx.x == 0) give_up(a);
+    return;
+  }
+  ZMI_ASTAMP(0);
+  const uint32_t tag = (uint32_t)pos + 1u;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c16 = lane & 15, h4 = lane >> 4;
+  const int kvr = a.kv_row ? a.kv_row[qi] : qi;
+  const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
+  const int nk = pos + 1, n32 = (pos + 32) >> 5, nc = pos / CH + 1;
+  const int c = wave;                      // this wave's chunk
+  const bool live = c < nc;
+  uint64_t* gu = gran + (size_t)unit * GRAN_STRIDE;
+
+  // (1) the chunk's cached K rows (positions < pos; the row of pos comes from the granules) and the
+  // V^T fragments of its four 32-key groups for dim slice s, all in flight at once
+  const int pc = max(pos - 1, 0);
+  uint4 kf[CPG][2][4], vf[CPG][DT];
+  if (live) {
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4) {
+      const int k = CPG * c + q4;
+      if (k < n32) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const bf16_t* kr = a.k + kvbase + (size_t)min(32 * k + 16 * tt + c16, pc) * HD + 8 * h4;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) kf[q4][tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
+        }
+      }
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4) {
+      const int k = CPG * c + q4;
+      if (k < n32) {
+        const int p0 = min(32 * k + 8 * h4, pos & ~7);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          vf[q4][dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * (DT * s + dt) + c16) * a.smax + p0);
+      }
+    }
+  }
+  if (wave == XR_POLL) {
+    // (2) this position's q, K row and V row (QKV_GRAN pairs; 6 per lane), two sweeps in flight
+    uint64_t A[6], B[6];
+    auto sweep = [&](uint64_t(&g)[6]) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) g[i] = ld_wt64(gu + lane + 64 * i);
+    };
+    auto ready = [&](const uint64_t(&g)[6]) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) ok = ok && tag_of(g[i]) == tag;
+      return __all(ok);
+    };
+    auto stage = [&](const uint64_t(&g)[6]) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) qkv_lds[lane + 64 * i] = (uint32_t)g[i];
+    };
+    sweep(A);
+    __builtin_amdgcn_s_sleep(8);
+    sweep(B);
+    for (unsigned spins = 0;; spins += 2) {
+      if (ready(A)) {
+        stage(A);
+        break;
+      }
+      sweep(A);
+      __builtin_amdgcn_s_sleep(8);
+      if (ready(B)) {
+        stage(B);
+        break;
+      }
+      sweep(B);
+      __builtin_amdgcn_s_sleep(8);
+      if (spins > XS_SPIN) {
+        give_up(a);
+        stage(A);
+        break;
+      }
+    }
+    ZMI_ASTAMP(1);
+  }
+  __syncthreads();
+
+  // (3) scores of the chunk: q from LDS, the K row / V^T slot of pos patched in, the chunked kernel's
+  // 4-MFMA chain per 16 keys; then the chunk maximum per head (exact in any order)
+  if (live) {
+    const uint4* q4p = reinterpret_cast<const uint4*>(qkv_lds);
+    uint4 qf[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+      qf[db] = c16 < XG ? q4p[(c16 * HD + 8 * h4 + 32 * db) >> 3] : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4)
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+        if (32 * (CPG * c + q4) + 16 * tt + c16 == pos) {
+#pragma unroll
+          for (int db = 0; db < 4; ++db) kf[q4][tt][db] = q4p[(XG * HD + 8 * h4 + 32 * db) >> 3];
+        }
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4) {
+      const int kb = 32 * (CPG * c + q4) + 8 * h4;
+      if (kb <= pos && pos < kb + 8) {
+        const int sl = pos - kb, wi = sl >> 1, sh = (sl & 1) * 16;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int d = 16 * (DT * s + dt) + c16;
+          const uint32_t pr = qkv_lds[(XG + 1) * HD / 2 + (d >> 1)];
+          const uint32_t val = (d & 1) ? (pr >> 16) : (pr & 0xffffu);
+          uint32_t w[4] = {vf[q4][dt].x, vf[q4][dt].y, vf[q4][dt].z, vf[q4][dt].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e == wi) w[e] = (w[e] & ~(0xffffu << sh)) | (val << sh);
+          vf[q4][dt] = uint4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4) {
+      const int k = CPG * c + q4;
+      if (k < n32) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          f32x4_t sv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int db = 0; db < 4; ++db) sv = mfma16(qf[db], kf[q4][tt][db], sv);
+          const int key = 32 * k + 16 * tt + c16;
+          if (h4 == 0 && key <= pos) {
+#pragma unroll
+            for (int i = 0; i < XG; ++i) sc[i][key] = sv[i] * a.scale;
+          }
+        }
+      }
+    }
+    ZMI_ASTAMP(2);
+    asm volatile("" ::: "memory");  // this wave's LDS writes stay ahead of its reads below (LDS is in order per wave)
+    float m[XG];
+#pragma unroll
+    for (int g = 0; g < XG; ++g) {
+      const int k0 = c * CH + lane;
+      m[g] = fmaxf(k0 < nk ? sc[g][k0] : -INFINITY, k0 + 64 < nk ? sc[g][k0 + 64] : -INFINITY);
+    }
+#pragma unroll
+    for (int g = 0; g < XG; ++g) m[g] = wave_max(m[g]);
+    if (lane == 0) {
+#pragma unroll
+      for (int g = 0; g < XG; ++g) mjc[c][g] = m[g];
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(3);
+
+  // (4) M_j = max over the chunks of blocks 0..j; e = exp(s - M_j), l, P = bf16(e); then P.V of the
+  // slice's dims, the chunk's four groups summed in group order in registers
+  if (live) {
+    const int j = c / CPB, dep = min((j + 1) * CPB, nc);
+    float l[XG];
+#pragma unroll
+    for (int g = 0; g < XG; ++g) {
+      float M = mjc[0][g];
+#pragma unroll
+      for (int cc = 1; cc < XR_CH; ++cc)
+        if (cc < dep) M = fmaxf(M, mjc[cc][g]);
+      if (c % CPB == 0 && lane == 0) mblk[j][g] = M;
+      l[g] = 0.f;
+#pragma unroll
+      for (int ii = 0; ii < CH / 64; ++ii) {
+        const int key = c * CH + lane + 64 * ii;
+        const float e = key < nk ? expf(sc[g][key] - M) : 0.f;
+        l[g] += e;
+        pb[g][key] = (bf16_t)f2bf(e);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < XG; ++g) l[g] = wave_sum(l[g]);
+    if (lane == 0) {
+#pragma unroll
+      for (int g = 0; g < XG; ++g) ljc[c][g] = l[g];
+    }
+    ZMI_ASTAMP(4);
+    asm volatile("" ::: "memory");
+    f32x4_t oc[DT];
+#pragma unroll
+    for (int q4 = 0; q4 < CPG; ++q4) {
+      const int k = CPG * c + q4;
+      if (k < n32) {
+        uint4 pf = uint4{0u, 0u, 0u, 0u};
+        if (c16 < XG) pf = *reinterpret_cast<const uint4*>(&pb[c16][32 * k + 8 * h4]);
+        const int kbase = 32 * k + 8 * h4;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          uint4 v = vf[q4][dt];
+          if (kbase + 8 > nk) {
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t lo = kbase + 2 * e < nk ? 0x0000ffffu : 0u;
+              const uint32_t hi = kbase + 2 * e + 1 < nk ? 0xffff0000u : 0u;
+              w[e] &= lo | hi;
+            }
+            v = uint4{w[0], w[1], w[2], w[3]};
+          }
+          const f32x4_t o = mfma16(pf, v, f32x4_t{0.f, 0.f, 0.f, 0.f});
+          if (q4 == 0) {
+            oc[dt] = o;
+          } else {
+            oc[dt][0] += o[0];
+            oc[dt][1] += o[1];
+            oc[dt][2] += o[2];
+            oc[dt][3] += o[3];
+          }
+        }
+      }
+    }
+    if (h4 == 0) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < XG; ++i) ocs[c][i][16 * dt + c16] = oc[dt][i];
+    }
+  }
+  __syncthreads();
+  ZMI_ASTAMP(5);
+  // (5) the block recursion (zmi_attn_merge.h), one thread per (head, dim of the slice)
+  if (t < XG * DSD) {
+    const int g = t / DSD, dl = t - g * DSD;
+    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
+    float ocv[XR_CH], lcv[XR_CH];
+#pragma unroll
+    for (int cc = 0; cc < XR_CH; ++cc) {
+      const int cr = min(cc, nc - 1);
+      ocv[cc] = ocs[cr][g][dl];
+      lcv[cc] = ljc[cr][g];
+    }
+#pragma unroll
+    for (int cc = 0; cc < XR_CH; ++cc) {
+      if (cc >= nc) break;
+      const float o = ocv[cc];
+      if (cc % CPB == 0) {
+        ob = o;
+        lb = lcv[cc];
+        mb = mblk[cc / CPB][g];
+      } else {
+        ob += o;
+        lb += lcv[cc];
+      }
+      if (cc % CPB == CPB - 1 || cc == nc - 1) {
+        if (cc < CPB) {
+          acc = ob;
+          l = lb;
+        } else {
+          const float et = expf(mprev - mb);
+          l = lb + et * l;
+          acc = acc * et + ob;
+        }
+        mprev = mb;
+      }
+    }
+    const float rl = 1.0f / l;
+    a.out[(size_t)qi * a.ldo + (kh * XG + g) * HD + DSD * s + dl] = (bf16_t)f2bf(acc * rl);
+  }
+  ZMI_ASTAMP(6);
+}
+
+// ---- chunk-split form (ZMI_ATTNBLK_SPLIT): one workgroup per 128-key chunk -----------------------
+// Workgroup c of a (query, kv head) loads only chunk c's K rows and V^T columns (64 KB: the cached K / V
+// of a query are read once, spread over its chunks' CUs), computes the chunk's scores, maximum,
+// e / l / P and P.V for all 128 dims: the chunked kernel's (zmi_attn.hip) per-chunk arithmetic. Two
+// granule hand-offs between the chunks of a query, both small: the chunk maxima (4 per chunk: M_j of
+// the chunk's block), then each chunk's P.V partial, l and M_j, of which workgroup c merges dims
+// 16 c .. 16 c + 15 (zmi_attn_merge.h's recursion). Workgroups of chunks past the position only merge.
+// Positions < XC_KEYS. Granules (after the unit's q / K / V pairs, tag = position + 1): GM [chunk][head]
+// maxima, GL [chunk][head] l, GB [chunk][head] M_j, GO [chunk][head][dim] P.V partials.
+constexpr int XC_CH = 8;                  // chunk workgroups per (query, kv head)
+constexpr int XC_KEYS = XC_CH * CH;       // 1024 keys (positions 0 .. 1023)
+constexpr int XC_GM = 0, XC_GL = XC_GM + XC_CH * XG, XC_GB = XC_GL + XC_CH * XG, XC_GO = XC_GB + XC_CH * XG;
+constexpr int XC_GWORDS = XC_GO + XC_CH * XG * HD;
+static_assert(XC_GWORDS <= XG * DS_KEYS, "the chunk-split granules share the score-granule area");
+static_assert(CH == 128 && DNW == 8, "eight waves: one 16-key score tile each over a 128-key chunk");
+
+struct XcImg {
+  static constexpr size_t SC = 0;                              // float [XG][CH] scores of the chunk
+  static constexpr size_t PB = SC + (size_t)XG * CH * 4;       // bf16  [XG][CH] P
+  static constexpr size_t OP = PB + (size_t)XG * CH * 2;       // float [CPG][XG][HD] per-group P.V
+  static constexpr size_t MJ = OP + (size_t)CPG * XG * HD * 4; // float [XG] M_j of the chunk's block
+  static constexpr size_t QKV = MJ + (size_t)XG * 4;           // u32 [QKV_GRAN] q | k | v pairs of pos
+  static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
+};
+
+__device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
+  float(&sc)[XG][CH] = *reinterpret_cast<float(*)[XG][CH]>(smem + XcImg::SC);
+  bf16_t(&pb)[XG][CH] = *reinterpret_cast<bf16_t(*)[XG][CH]>(smem + XcImg::PB);
+  float(&opart)[CPG][XG][HD] = *reinterpret_cast<float(*)[CPG][XG][HD]>(smem + XcImg::OP);
+  float* mj = reinterpret_cast<float*>(smem + XcImg::MJ);
+  uint32_t* qkv_lds = reinterpret_cast<uint32_t*>(smem + XcImg::QKV);
+
+  const int y = b >> 3;
+  const int c = y % XC_CH, unit = 8 * (y / XC_CH) + (b & 7);
+  if (unit >= n_units) return;
+  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
+  const int pos = a.pos[qi];
+  if (pos < 0) return;
+  if (pos >= XC_KEYS) {  // the engine never launches this form past its capacity; refuse, don't read past it
+    if (threadIdx.x == 0) give_up(a);
+    return;
+  }
+  ZMI_ASTAMP(0);
+  const uint32_t tag = (uint32_t)pos + 1u;
+  const uint64_t tag64 = (uint64_t)tag << 32;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c16 = lane & 15, h4 = lane >> 4;
+  const int nk = pos + 1, n32 = (pos + 32) >> 5, nc = pos / CH + 1;
+  uint64_t* gu = gran + (size_t)unit * GRAN_STRIDE;
+  uint64_t* gx = gu + QKV_GRAN;
+
+  if (c < nc) {
+    const int kvr = a.kv_row ? a.kv_row[qi] : qi;
+    const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
+    // (1) wave w: score tile (group w >> 1, 16 keys w & 1) K rows and the V^T fragments of group w & 3,
+    // dims 64 (w >> 2) .. + 63, positions < pos (the row of pos comes from the granules)
+    const int gs = wave >> 1, tt = wave & 1, gv = wave & 3, hv = wave >> 2;
+    const int pc = max(pos - 1, 0);
+    const bool sk = CPG * c + gs < n32, vk = CPG * c + gv < n32;
+    uint4 kf[4], vf[4];
+    if (sk) {
+      const bf16_t* kr = a.k + kvbase + (size_t)min(CH * c + 32 * gs + 16 * tt + c16, pc) * HD + 8 * h4;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) kf[db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
+    }
+    if (vk) {
+      const int p0 = min(CH * c + 32 * gv + 8 * h4, pos & ~7);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(64 * hv + 16 * dt + c16) * a.smax + p0);
+    }
+    if (wave == 0) {
+      // (2) this position's q, K row and V row (QKV_GRAN pairs; 6 per lane), two sweeps in flight
+      uint64_t A[6], B[6];
+      auto sweep = [&](uint64_t(&g)[6]) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) g[i] = ld_wt64(gu + lane + 64 * i);
+      };
+      auto ready = [&](const uint64_t(&g)[6]) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) ok = ok && tag_of(g[i]) == tag;
+        return __all(ok);
+      };
+      auto stage = [&](const uint64_t(&g)[6]) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) qkv_lds[lane + 64 * i] = (uint32_t)g[i];
+      };
+      sweep(A);
+      __builtin_amdgcn_s_sleep(8);
+      sweep(B);
+      for (unsigned spins = 0;; spins += 2) {
+        if (ready(A)) {
+          stage(A);
+          break;
+        }
+        sweep(A);
+        __builtin_amdgcn_s_sleep(8);
+        if (ready(B)) {
+          stage(B);
+          break;
+        }
+        sweep(B);
+        __builtin_amdgcn_s_sleep(8);
+        if (spins > XS_SPIN) {
+          give_up(a);
+          stage(A);
+          break;
+        }
+      }
+      ZMI_ASTAMP(1);
+    }
+    __syncthreads();
+    // (3) the tile's scores (the chunked kernel's 4-MFMA chain; the K row of pos patched in)
+    const uint4* q4p = reinterpret_cast<const uint4*>(qkv_lds);
+    if (sk) {
+      uint4 qf[4];
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+        qf[db] = c16 < XG ? q4p[(c16 * HD + 8 * h4 + 32 * db) >> 3] : uint4{0u, 0u, 0u, 0u};
+      const int key = CH * c + 32 * gs + 16 * tt + c16;
+      if (key == pos) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db) kf[db] = q4p[(XG * HD + 8 * h4 + 32 * db) >> 3];
+      }
+      f32x4_t sv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int db = 0; db < 4; ++db) sv = mfma16(qf[db], kf[db], sv);
+      if (h4 == 0 && key <= pos) {
+#pragma unroll
+        for (int i = 0; i < XG; ++i) sc[i][key - CH * c] = sv[i] * a.scale;
+      }
+    }
+    if (vk) {  // the V^T slot of pos, in the fragment whose 8 positions hold it
+      const int kb = CH * c + 32 * gv + 8 * h4;
+      if (kb <= pos && pos < kb + 8) {
+        const int sl = pos - kb, wi = sl >> 1, sh = (sl & 1) * 16;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int d = 64 * hv + 16 * dt + c16;
+          const uint32_t pr = qkv_lds[(XG + 1) * HD / 2 + (d >> 1)];
+          const uint32_t val = (d & 1) ? (pr >> 16) : (pr & 0xffffu);
+          uint32_t w[4] = {vf[dt].x, vf[dt].y, vf[dt].z, vf[dt].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e == wi) w[e] = (w[e] & ~(0xffffu << sh)) | (val << sh);
+          vf[dt] = uint4{w[0], w[1], w[2], w[3]};
+        }
+      }
+    }
+    __syncthreads();
+    ZMI_ASTAMP(2);
+    // (4) wave 0: the chunk maxima (exact in any order) out as granules, then M_j of the chunk's block
+    // from the maxima of chunks 0 .. dep - 1 (lane = chunk x XG + head)
+    if (wave == 0) {
+      float m[XG];
+#pragma unroll
+      for (int g = 0; g < XG; ++g)
+        m[g] = fmaxf(CH * c + lane < nk ? sc[g][lane] : -INFINITY, CH * c + lane + 64 < nk ? sc[g][lane + 64] : -INFINITY);
+#pragma unroll
+      for (int g = 0; g < XG; ++g) m[g] = wave_max(m[g]);
+      if (lane < XG) {
+        const float mine = lane == 0 ? m[0] : (lane == 1 ? m[1] : (lane == 2 ? m[2] : m[3]));
+        st_wt64(gx + XC_GM + c * XG + lane, (uint64_t)__float_as_uint(mine) | tag64);
+      }
+      const int j = c / CPB, dep = min((j + 1) * CPB, nc);
+      const int cc = lane / XG, g = lane - cc * XG;
+      float v = -INFINITY;
+      if (lane < dep * XG) {
+        if (cc == c) {
+          v = g == 0 ? m[0] : (g == 1 ? m[1] : (g == 2 ? m[2] : m[3]));
+        } else {
+          uint64_t w = ld_wt64(gx + XC_GM + lane);
+          for (unsigned spins = 0; tag_of(w) != tag; ++spins) {
+            if (spins > XS_SPIN) {
+              give_up(a);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            w = ld_wt64(gx + XC_GM + lane);
+          }
+          v = __uint_as_float((uint32_t)w);
+        }
+      }
+      // max over the chunks of each head: lanes g, g + 4, ..., g + 28 (dep <= 8 chunks)
+      v = fmaxf(v, __shfl_xor(v, 4));
+      v = fmaxf(v, __shfl_xor(v, 8));
+      v = fmaxf(v, __shfl_xor(v, 16));
+      if (lane < XG) mj[lane] = v;
+    }
+    __syncthreads();
+    ZMI_ASTAMP(3);
+    // (5) waves 0..3 (head w): e = exp(s - M_j), l (lane L: keys L, L + 64, then wave_sum), P = bf16(e)
+    if (wave < XG) {
+      const float M = mj[wave];
+      float l = 0.f;
+#pragma unroll
+      for (int ii = 0; ii < CH / 64; ++ii) {
+        const int kk = lane + 64 * ii;
+        const float e = CH * c + kk < nk ? expf(sc[wave][kk] - M) : 0.f;
+        l += e;
+        pb[wave][kk] = (bf16_t)f2bf(e);
+      }
+      l = wave_sum(l);
+      if (lane == 0) {
+        st_wt64(gx + XC_GL + c * XG + wave, (uint64_t)__float_as_uint(l) | tag64);
+        st_wt64(gx + XC_GB + c * XG + wave, (uint64_t)__float_as_uint(M) | tag64);
+      }
+    }
+    __syncthreads();
+    ZMI_ASTAMP(4);
+    // (6) P.V of group w & 3 for dims 64 (w >> 2) .. + 63 (V of keys past the position zeroed)
+    if (vk) {
+      uint4 pf = uint4{0u, 0u, 0u, 0u};
+      if (c16 < XG) pf = *reinterpret_cast<const uint4*>(&pb[c16][32 * gv + 8 * h4]);
+      const int kbase = CH * c + 32 * gv + 8 * h4;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        uint4 v = vf[dt];
+        if (kbase + 8 > nk) {
+          uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t lo = kbase + 2 * e < nk ? 0x0000ffffu : 0u;
+            const uint32_t hi = kbase + 2 * e + 1 < nk ? 0xffff0000u : 0u;
+            w[e] &= lo | hi;
+          }
+          v = uint4{w[0], w[1], w[2], w[3]};
+        }
+        const f32x4_t o = mfma16(pf, v, f32x4_t{0.f, 0.f, 0.f, 0.f});
+        if (h4 == 0) {
+#pragma unroll
+          for (int i = 0; i < XG; ++i) opart[gv][i][64 * hv + 16 * dt + c16] = o[i];
+        }
+      }
+    }
+    __syncthreads();
+    // (7) the chunk's P.V (groups summed in group order) out as granules, one (head, dim) per thread
+    {
+      const int g = t / HD, d = t - g * HD;
+      float o = opart[0][g][d];
+#pragma unroll
+      for (int w = 1; w < CPG; ++w)
+        if (CPG * c + w < n32) o += opart[w][g][d];
+      st_wt64(gx + XC_GO + (c * XG + g) * HD + d, (uint64_t)__float_as_uint(o) | tag64);
+    }
+    ZMI_ASTAMP(5);
+  }
+  // (8) dims 16 c .. + 15 of the unit's output: every chunk's partial, l and M_j (gathered), the block
+  // recursion of zmi_attn_merge.h, one thread per (head, dim)
+  if (t < XG * 16) {
+    const int g = t >> 4, d = 16 * c + (t & 15);
+    uint64_t ov[XC_CH], lv[XC_CH], mv[XC_CH / CPB];
+    unsigned pend = 0;
+#pragma unroll
+    for (int k = 0; k < XC_CH; ++k)
+      if (k < nc) pend |= 3u << (2 * k);
+#pragma unroll
+    for (int j = 0; j < XC_CH / CPB; ++j)
+      if (j * CPB < nc) pend |= 1u << (2 * XC_CH + j);
+    for (unsigned spins = 0; pend; ++spins) {
+#pragma unroll
+      for (int k = 0; k < XC_CH; ++k) {
+        if ((pend >> (2 * k)) & 1) ov[k] = ld_wt64(gx + XC_GO + (k * XG + g) * HD + d);
+        if ((pend >> (2 * k + 1)) & 1) lv[k] = ld_wt64(gx + XC_GL + k * XG + g);
+      }
+#pragma unroll
+      for (int j = 0; j < XC_CH / CPB; ++j)
+        if ((pend >> (2 * XC_CH + j)) & 1) mv[j] = ld_wt64(gx + XC_GB + j * CPB * XG + g);
+#pragma unroll
+      for (int k = 0; k < XC_CH; ++k) {
+        if (((pend >> (2 * k)) & 1) && tag_of(ov[k]) == tag) pend &= ~(1u << (2 * k));
+        if (((pend >> (2 * k + 1)) & 1) && tag_of(lv[k]) == tag) pend &= ~(1u << (2 * k + 1));
+      }
+#pragma unroll
+      for (int j = 0; j < XC_CH / CPB; ++j)
+        if (((pend >> (2 * XC_CH + j)) & 1) && tag_of(mv[j]) == tag) pend &= ~(1u << (2 * XC_CH + j));
+      if (!pend) break;
+      if (spins > XS_SPIN) {
+        give_up(a);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
+#pragma unroll
+    for (int k = 0; k < XC_CH; ++k) {
+      if (k >= nc) break;
+      const float o = __uint_as_float((uint32_t)ov[k]), lk = __uint_as_float((uint32_t)lv[k]);
+      if (k % CPB == 0) {
+        ob = o;
+        lb = lk;
+        mb = __uint_as_float((uint32_t)mv[k / CPB]);
+      } else {
+        ob += o;
+        lb += lk;
+      }
+      if (k % CPB == CPB - 1 || k == nc - 1) {
+        if (k < CPB) {
+          acc = ob;
+          l = lb;
+        } else {
+          const float et = expf(mprev - mb);
+          l = lb + et * l;
+          acc = acc * et + ob;
+        }
+        mprev = mb;
+      }
+    }
+    const float rl = 1.0f / l;
+    a.out[(size_t)qi * a.ldo + (kh * XG + g) * HD + d] = (bf16_t)f2bf(acc * rl);
+  }
+  ZMI_ASTAMP(6);
+}
+
 // PRO: the projection's prologue, LayerNorm (transformer blocks) or ADDLN (the hybrid's MHA blocks:
-// layer_norm_fn(hidden, residual) with the new residual written by column block 0)
-template <int S, int PRO>
+// layer_norm_fn(hidden, residual) with the new residual written by column block 0). SELF: the
+// attention role is xr_body (self-scoring) instead of xs_body (score exchange).
+template <int S, int PRO, int FORM>
 __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
                                                         int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -448,29 +1081,35 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
   if (b < n_qkv)
     zmi_gemv::gemv_body<QG, QW, QNL, QRT, PRO, ZMI_EPI_QKV, 1, 1>(
         qa, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, GRAN_STRIDE});
-  else if (b < n_qkv + n_xs)
-    xs_body<S>(at, n_units, b - n_qkv, smem, gran);
-  else
+  else if (b < n_qkv + n_xs) {
+    if constexpr (FORM == FORM_SELF)
+      xr_body<S>(at, n_units, b - n_qkv, smem, gran);
+    else if constexpr (FORM == FORM_SPLIT)
+      xc_body(at, n_units, b - n_qkv, smem, gran);
+    else
+      xs_body<S>(at, n_units, b - n_qkv, smem, gran);
+  } else
     prefetch_body<NT>(pf, b - n_qkv - n_xs, n_pf);
 }
 
-template <int S, int PRO>
+template <int S, int PRO, int FORM>
 hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArgs& at, int n_units, uint64_t* gran,
                         const ZmiPrefetch& pf, hipStream_t s) {
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
-  const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, PRO), XsImg<S>::BYTES,
+  const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, PRO),
+                               FORM == FORM_SELF ? XrImg<S>::BYTES : (FORM == FORM_SPLIT ? XcImg::BYTES : XsImg<S>::BYTES),
                                zmi_gemv::LDS_MAX / 2 + 1024});
   if (lds > zmi_gemv::LDS_MAX) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S, PRO>),
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S, PRO, FORM>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)zmi_gemv::LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
   const int n_xs = (n_units + 7) / 8 * 8 * S;
   const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
-  hipLaunchKernelGGL((attn_block_kernel<S, PRO>), dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
+  hipLaunchKernelGGL((attn_block_kernel<S, PRO, FORM>), dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
                      n_units, gran, pf, n_pf);
   return hipGetLastError();
 }
@@ -493,7 +1132,6 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   if (a.hd != HD || a.hkv <= 0 || a.hq != XG * a.hkv)
     return zmi_fail_msg("attn_block: head_dim 128, 4 query heads per kv head");
   if (a.N != (a.hq + 2 * a.hkv) * a.hd || a.n_valid != a.N) return zmi_fail_msg("attn_block: N = (hq + 2 hkv) hd");
-  if (a.smax - 1 >= DS_KEYS) return zmi_fail_msg("attn_block: positions must stay below zmi_attention_max_keys_whole()");
   if (a.smax % 8 || !a.row_pos || !a.row_kv || !a.rope || !a.k_cache || !a.v_cache || !gran || !err || !attn_out)
     return zmi_fail_msg("attn_block: missing buffers (or smax % 8)");
   if (ldo % 8 || a.ldx % 8) return zmi_fail_msg("attn_block: ldo / ldx must be multiples of 8");
@@ -526,15 +1164,24 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   hipError_t e;
   using zmi_gemv::PRO_ADDLN;
   using zmi_gemv::PRO_LN;
-  if (slices != 4 && slices != 8) return zmi_fail_msg("attn_block: slices must be 4 or 8");
-  if (addln)
-    e = slices == 4 ? launch_block<4, PRO_ADDLN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
-                    : launch_block<8, PRO_ADDLN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s);
-  else
-    e = slices == 4 ? launch_block<4, PRO_LN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
-                    : launch_block<8, PRO_LN>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s);
+  const int form = (slices & ZMI_ATTNBLK_SPLIT) ? FORM_SPLIT : ((slices & ZMI_ATTNBLK_SELF) ? FORM_SELF : FORM_XS);
+  const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
+  if (form == FORM_SPLIT ? sl != 8 : (sl != 4 && sl != 8))
+    return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 | ZMI_ATTNBLK_SPLIT");
+#define ZMI_BLK(S_, P_, F_) launch_block<S_, P_, F_>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
+#define ZMI_BLK_P(P_)                                                                                \
+  (form == FORM_SPLIT ? ZMI_BLK(8, P_, FORM_SPLIT)                                                   \
+                      : form == FORM_SELF ? (sl == 4 ? ZMI_BLK(4, P_, FORM_SELF) : ZMI_BLK(8, P_, FORM_SELF)) \
+                                          : (sl == 4 ? ZMI_BLK(4, P_, FORM_XS) : ZMI_BLK(8, P_, FORM_XS)))
+  e = addln ? ZMI_BLK_P(PRO_ADDLN) : ZMI_BLK_P(PRO_LN);
+#undef ZMI_BLK_P
+#undef ZMI_BLK
   ZMI_CHECK(e);
   return 0;
+}
+
+extern "C" int zmi_attn_block_max_pos(int slices) {
+  return (slices & ZMI_ATTNBLK_SPLIT) ? XC_KEYS - 1 : ((slices & ZMI_ATTNBLK_SELF) ? XR_KEYS - 1 : DS_KEYS - 1);
 }
 
 extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,

@@ -489,7 +489,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   } else if (EPI == ZMI_EPI_QKV) {
     // q | k | v split, interleaved-pair RoPE in fp32 on q and k, KV-cache write (_torch.py:18-49,117-126)
     const int r = lane >> 2, c = (lane & 3) * 2;
-    if (r < rows && q_pos >= 0) {
+    if (r < rows && q_pos >= 0 && q_pos < a.smax) {  // the launchers check positions against smax; never write past it
       const int n = col0 + c;
       const int qcols = a.hq * a.hd, kcols = a.hkv * a.hd;
       float x0 = bfround(colsum(c, r)), x1 = bfround(colsum(c + 1, r));

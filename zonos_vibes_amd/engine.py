@@ -100,13 +100,22 @@ class HipEngine:
         # positions below the whole-query kernel's reach; identical bits either way (speed only)
         self.attn_block = True
         self.attn_block_slices = 8
+        # fused forms tried in order, each where every row's position is below its reach: "split" (one
+        # workgroup per 128-key chunk, positions < 1024), "self" (every slice scores all keys, < 1024),
+        # "xs" (slices exchange scores, < 1280); beyond, separate launches. The form is picked per run
+        # of steps from host-side position bounds; all forms give identical bits
+        self.attn_forms = ("split", "xs")
+        self.attn_self_slices = 8
         # prefetch-only workgroups in that launch warm the Infinity Cache with out_proj's weights and the
         # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only)
         self.prefetch_blocks = 192
         self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
-        self._plans: dict[int, list] = {}
-        self._graphs: dict[int, int] = {}
+        self._plans: dict[tuple, list] = {}
+        self._graphs: dict[tuple, int] = {}
+        # host-side upper bound of each slot's next decode position (prefill sets it, every step adds 1):
+        # it picks the attention form of a run of steps without reading the device
+        self.pos_hi = [0] * self.S
         self.n_kv = self._kv_layers()
         self._alloc()
 
@@ -243,18 +252,51 @@ class HipEngine:
         self._graphs.clear()
         self._plans.clear()
 
-    def _use_attn_block(self, rows: int) -> bool:
-        return (self.attn_block and rows <= 16 and self.d == 2048 and self.H == 4 * self.Hkv
-                and self.smax - 1 < self.lib.zmi_attention_max_keys_whole())
+    def _block_slices(self, form: str) -> int:
+        """zmi_attn_block `slices` argument of a fused form."""
+        if form == "split":
+            return 8 | _lib.ATTNBLK_SPLIT
+        return self.attn_self_slices | _lib.ATTNBLK_SELF if form == "self" else self.attn_block_slices
 
-    def _plan(self, rows: int) -> list:
+    def _forms(self, rows: int) -> list:
+        """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
+        QKV and attention launches (any position)."""
+        out = []
+        if self.attn_block and rows <= 16 and self.d == 2048 and self.H == 4 * self.Hkv:
+            for f in self.attn_forms:
+                out.append((f, self.lib.zmi_attn_block_max_pos(self._block_slices(f))))
+        return out + [("none", 1 << 30)]
+
+    def _use_attn_block(self, rows: int, form: str | None = None) -> bool:
+        return form != "none" and any(f == form for f, _ in self._forms(rows))
+
+    def _segments(self, n: int, slots: int) -> list:
+        """Split a run of n decode steps of slots 0..slots-1 into (steps, form) pieces: each piece's
+        positions (host bound pos_hi .. + steps - 1) stay within its form's reach."""
+        rows = 2 * slots
+        p0 = max(self.pos_hi[:slots])
+        segs = []
+        while n > 0:
+            for form, last in self._forms(rows):
+                if p0 <= last:
+                    k = min(n, last - p0 + 1)
+                    break
+            if segs and segs[-1][1] == form:
+                segs[-1] = (segs[-1][0] + k, form)
+            else:
+                segs.append((k, form))
+            n -= k
+            p0 += k
+        return segs
+
+    def _plan(self, rows: int, form: str = "none") -> list:
         """Decode-step launches for the first `rows` rows (slots 0 .. rows/2 - 1). Every kernel's
         per-row arithmetic is independent of `rows` and of the launch form, so a slot decodes
         identically in any plan."""
-        if rows not in self._plans:
+        if (rows, form) not in self._plans:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
-            fused = self._use_attn_block(rows)
+            fused = self._use_attn_block(rows, form)
             # past a few rows every column-block workgroup's LayerNorm of all of them costs more than the
             # launch that normalises them once per layer (fc1 at 16 rows: 30.7 us with the prologue);
             # zmi_layernorm_rows gives the prologue's bits, so the plan may switch at any row count
@@ -282,7 +324,7 @@ class HipEngine:
                         pf.ptr[1] = lw["fc1"].data_ptr()
                         pf.bytes[1] = min(lw["fc1"].numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
                         pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
-                    plan.append(("attnblk", (qkv[0], i, pf)))
+                    plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form))))
                 else:
                     plan.append(("gemv", qkv))
                     plan.append(("attn", i))
@@ -296,8 +338,8 @@ class HipEngine:
                                n_valid=HEADS_N, ln=ln)
             heads[0].groups = self.heads_groups
             plan.append(("gemv", heads))
-            self._plans[rows] = plan
-        return self._plans[rows]
+            self._plans[(rows, form)] = plan
+        return self._plans[(rows, form)]
 
     def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
         _lib.check(self.lib.zmi_attention_variant(
@@ -307,9 +349,9 @@ class HipEngine:
             "attention")
 
     def _run_attn_block(self, item):
-        a, i, pf = item
+        a, i, pf, slices = item
         _lib.check(self.lib.zmi_attn_block_pf(ctypes.byref(a), self.blk_gran[i].data_ptr(), self.blk_err.data_ptr(),
-                                              self.attn.data_ptr(), self.H * self.hd, self.attn_block_slices,
+                                              self.attn.data_ptr(), self.H * self.hd, slices,
                                               ctypes.byref(pf), self.sptr), "attn_block")
 
     def check_errors(self):
@@ -339,12 +381,16 @@ class HipEngine:
             raise ValueError(f"slots {s} outside 1..{self.S}")
         return 2 * s
 
-    def enqueue_step(self, noise: torch.Tensor | None = None, slots: int | None = None):
+    def enqueue_step(self, noise: torch.Tensor | None = None, slots: int | None = None, form: str | None = None):
         """One decode step for slots 0 .. slots-1 (default: all; reference model.py:276-307), enqueued
         on self.stream. The step's input embeddings and (kv row, position) tables were written by
-        the previous sampler launch (or the prefill's), fused into its frame-write epilogue."""
+        the previous sampler launch (or the prefill's), fused into its frame-write epilogue.
+        form: the attention form (default: from the slots' position bounds; the bound advances)."""
         rows = self._rows(slots)
-        for kind, item in self._plan(rows):
+        if form is None:
+            form = self._segments(1, rows // 2)[0][1]
+            self._advance(1, rows // 2)
+        for kind, item in self._plan(rows, form):
             if kind == "gemv":
                 self._run_gemv(item)
             elif kind == "attnblk":
@@ -356,26 +402,35 @@ class HipEngine:
                 item()
         self._sample(self.logits, noise, 0, 0, rows // 2)
 
-    def capture(self, slots: int | None = None):
+    def capture(self, slots: int | None = None, form: str = "none"):
         rows = self._rows(slots)
-        if rows not in self._graphs:
+        if (rows, form) not in self._graphs:
             _lib.check(self.lib.zmi_graph_begin(self.sptr), "graph_begin")
             try:
-                self.enqueue_step(slots=rows // 2)
+                self.enqueue_step(slots=rows // 2, form=form)
             finally:
                 g = ctypes.c_void_p()
                 _lib.check(self.lib.zmi_graph_end(self.sptr, ctypes.byref(g)), "graph_end")
-            self._graphs[rows] = g.value
-        return self._graphs[rows]
+            self._graphs[(rows, form)] = g.value
+        return self._graphs[(rows, form)]
+
+    def _advance(self, n: int, slots: int):
+        for s in range(slots):
+            self.pos_hi[s] += n
 
     def step(self, n: int = 1, use_graph: bool = True, slots: int | None = None):
+        """n decode steps of slots 0 .. slots-1, as runs of hipGraph replays (one graph per attention
+        form: a run switches form where the slots' position bound crosses a form's reach)."""
         if n <= 0:
             return
-        if use_graph:
-            _lib.check(self.lib.zmi_graph_launch(self.capture(slots), n, self.sptr), "graph_launch")
-        else:
-            for _ in range(n):
-                self.enqueue_step(slots=slots)
+        s = self._rows(slots) // 2
+        for k, form in self._segments(n, s):
+            if use_graph:
+                _lib.check(self.lib.zmi_graph_launch(self.capture(s, form), k, self.sptr), "graph_launch")
+            else:
+                for _ in range(k):
+                    self.enqueue_step(slots=s, form=form)
+            self._advance(k, s)
 
     # ------------------------------------------------------------------ prefill
     def prefill(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
@@ -422,6 +477,7 @@ class HipEngine:
             for k, v in vals.items():
                 st[k][slot] = v
             self._sample(self.logits_pre, noise, 1, slot, 1)
+        self.pos_hi[slot] = s_len
         return s_len
 
     def _reset_granules(self, slot: int):
@@ -485,6 +541,7 @@ class HipEngine:
         return out.unsqueeze(0)
 
     def release(self, slot: int):
+        self.pos_hi[slot] = 0
         with torch.cuda.stream(self.stream):
             self.st["active"][slot] = 0
             self.row_pos[2 * slot: 2 * slot + 2] = -1

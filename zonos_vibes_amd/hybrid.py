@@ -243,14 +243,14 @@ class HybridEngine(HipEngine):
         a.pro, a.aux, a.ld_aux, a.res_out = pro, aux.data_ptr(), ld_aux, _lib.ptr(res_out)
         return ("gemv", (a, epi))
 
-    def _plan(self, rows: int) -> list:
+    def _plan(self, rows: int, form: str = "none") -> list:
         """Decode launches. The block norms run as GEMV prologues: layer_norm_fn(hidden, residual) as ADDLN
         on the consuming GEMV (in_proj / qkv / fc1 / heads; the new residual goes to the other of two
         buffers, since the other workgroups still read the old one), RMSNormGated as GRMS on out_proj (up
         to 4 rows, the gate z * sigmoid(z) formed once per channel by the Mamba2 step kernel: the y and f32
         gate rows of a larger tile would not fit the LDS image). Same arithmetic as the
         prefill's standalone norm kernels."""
-        if rows not in self._plans:
+        if (rows, form) not in self._plans:
             w, d, md, qd = self.w, self.d, self.md, self.H * self.hd
             res = [self.x, self.x2]
             cur = 0
@@ -274,12 +274,12 @@ class HybridEngine(HipEngine):
                     qkv = normed_gemv(self._gemv(lw["qkv"], x_in, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                                  kv=(self.kc[j], self.vc[j]), row_kv=self.row_kv,
                                                  row_pos=self.row_pos), ln1, i == 0)
-                    if self._use_attn_block(rows):
+                    if self._use_attn_block(rows, form):
                         pf = _lib.Prefetch()
                         if self.prefetch_blocks > 0:  # out_proj's weights into the Infinity Cache meanwhile
                             pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
                             pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
-                        plan.append(("attnblk", (qkv[1][0], j, pf)))
+                        plan.append(("attnblk", (qkv[1][0], j, pf, self._block_slices(form))))
                     else:
                         plan.append(qkv)
                         plan.append(("attn", j))
@@ -315,8 +315,8 @@ class HybridEngine(HipEngine):
                                n_valid=HEADS_N)
             heads[0].ln_w, heads[0].ln_b = w["nf_w"].data_ptr(), w["nf_b"].data_ptr()
             plan.append(self._fused(heads, _lib.PRO_ADDLN, res[cur], d, None))
-            self._plans[rows] = plan
-        return self._plans[rows]
+            self._plans[(rows, form)] = plan
+        return self._plans[(rows, form)]
 
     # ------------------------------------------------------------------ prefill
     def _prefill_layers(self, m: int, max_pos: int):

@@ -192,6 +192,7 @@ class Zonos:
                     if not act[s]:
                         results[owner[s]] = e.read_codes(s)
                         owner[s] = -1
+                        e.pos_hi[s] = 0  # its rows are inactive (position -1): no bound on the attention form
             fill()
         return results
 
