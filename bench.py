@@ -34,9 +34,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 BASELINE_RTF = 2.0     # "~2x" real-time on RTX 4090 (README.md:84)
 
 
-def cond_tensor(seed: int, d: int, dev):
+def cond_tensor(seed: int, d: int, dev, lc: int = LC):
     import numpy as np
-    a = syn.synthetic_conditioning_np(seed, 2, LC, d)
+    a = syn.synthetic_conditioning_np(seed, 2, lc, d)
     return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
 
 
@@ -105,7 +105,75 @@ def time_decode_step(model, cond, steps: int = 64):
     return start.elapsed_time(end) * 1000.0 / steps, s_len + lead + steps // 2
 
 
+def kernel_table(model, cond, reps: int = 3) -> dict:
+    """Every kernel of the C2 decode step at the utterance's mean position, timed on the engine stream
+    with HIP events: the GEMVs as all 26 layers' launches back to back (each weight from HBM, as in the
+    step), the fused QKV + attention launch one launch at a time with its hand-off granules zeroed first
+    (a re-run at the same position would otherwise find its own granules and skip the wait), the sampler
+    alone. Per kernel: avg us per launch, algorithmic bytes per launch, GB/s and fraction of HBM peak."""
+    from zonos_vibes_amd.engine import SamplingParams
+    e = model.engine
+    s_len = e.prefill(0, cond, None, N_NEW, SamplingParams(temperature=0.0, cfg_scale=2.0))
+    lead = (N_NEW + 8) // 2
+    e.step(lead, slots=1)
+    pos = s_len + lead
+    form = e._segments(1, 1)[0][1]
+    plan = e._plan(2, form)
+    d, F, qkv_n = e.d, e.F, (e.H + 2 * e.Hkv) * e.hd
+    kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)  # K + V of both CFG rows, one layer
+    gem = [it for kd, it in plan if kd == "gemv"]
+    kinds = {
+        "out_proj": ([it for it in gem if it[1] == _lib.EPI_RESIDUAL][0::2], d * d * 2),
+        "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2),
+        "fc2": ([it for it in gem if it[1] == _lib.EPI_RESIDUAL][1::2], d * F * 2),
+        "heads (LN + logits)": ([it for it in gem if it[1] == _lib.EPI_LOGITS], 9 * 1025 * d * 2),
+    }
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {}
+    with torch.cuda.stream(e.stream):
+        for name, (items, nbytes) in kinds.items():
+            for it in items:
+                e._run_gemv(it)
+            st.record(e.stream)
+            for _ in range(reps):
+                for it in items:
+                    e._run_gemv(it)
+            en.record(e.stream)
+            en.synchronize()
+            us = st.elapsed_time(en) * 1000.0 / (reps * len(items))
+            out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
+                             hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items))
+        blk = [it for kd, it in plan if kd == "attnblk"]
+        if blk:
+            tot = 0.0
+            for _ in range(reps):
+                for it in blk:
+                    e.blk_gran[it[1]].zero_()
+                    st.record(e.stream)
+                    e._run_attn_block(it)
+                    en.record(e.stream)
+                    en.synchronize()
+                    tot += st.elapsed_time(en) * 1000.0
+            us = tot / (reps * len(blk))
+            nbytes = qkv_n * d * 2 + kv
+            out[f"attn_block ({form}: LN + QKV + RoPE + KV write + attention)"] = dict(
+                us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
+                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk),
+                note="QKV weights + the layer's K/V of both rows; the launch also prefetches out_proj's weights")
+        st.record(e.stream)
+        for _ in range(reps):
+            e._sample(e.logits, None, 0, 0, 1)
+        en.record(e.stream)
+        en.synchronize()
+        out["sampler (CFG + penalty + argmax + FSM + next embedding)"] = dict(
+            us=round(st.elapsed_time(en) * 1000.0 / reps, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
+    e.check_errors()
+    e.release(0)
+    return {"pos": pos, "kernels": out}
+
+
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA
+DAC_FLOP_PER_FRAME = 1_608_302_592  # SURVEY.md §8d: DacDecoder MACs x 2 per frame (hooks), 44.1 kHz dims
 
 
 def dac_encode_flop_per_frame() -> int:
@@ -297,6 +365,78 @@ def time_batch(model, dev, n_utt: int = 64, slots: int = 64) -> dict:
             "dac_s": round(t2 - t1, 3), "frames_per_s": round(frames / (t2 - t0), 1)}
 
 
+def c3_job(n_utt: int = 512) -> tuple[list[int], list[int]]:
+    """BASELINE config C3: 512 utterances, utterance i seeded by i: length uniform 2-30 s
+    (N = round(s * 44100 / 512) frames), Lc = 8 + round(15 s) conditioning rows. Returns (Lc, N) lists."""
+    lcs, n_new = [], []
+    for i in range(n_utt):
+        sec = 2.0 + 28.0 * float(torch.rand(1, generator=torch.Generator().manual_seed(i)))
+        lcs.append(8 + round(15 * sec))
+        n_new.append(max(1, round(sec * DAC_SAMPLE_RATE / DAC_HOP)))
+    return lcs, n_new
+
+
+def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) -> dict:
+    """C3 batch-sharded throughput (north_star): the first per_gpu x world of
+    the 512 C3 utterances (all 512 at 8 GPUs; per-GPU work fixed as the rank count grows), LPT-sharded
+    over the ranks with no communication (shard.generate_sharded: 64 continuous-batching slots per GPU),
+    DAC decode of every utterance on its rank, then the end-of-batch gather of the codes to rank 0
+    (int16 over RCCL). Aggregate real time = total audio s / max-over-ranks wall."""
+    from zonos_vibes_amd.shard import estimated_frames, generate_sharded, lpt_assign
+    d = model.config.backbone.d_model
+    lcs, n_all = c3_job()
+    n_utt = min(len(lcs), per_gpu * world)
+    lcs, n_new = lcs[:n_utt], n_all[:n_utt]
+    conds = [cond_tensor(1000 + i, d, dev, lc) for i, lc in enumerate(lcs)]
+    mine_plan = lpt_assign(estimated_frames(conds, [None] * n_utt, n_new), world)[rank]
+    # grow the engine to this job's capacity and capture its 64-slot graph outside the timed region
+    model._ensure_capacity(per_gpu, max(lcs) + max(n_new) + 9, max(lcs) + 1)
+    warm = min(per_gpu, n_utt)
+    model.generate_batch(conds[:warm], max_new_tokens=[4] * warm, sampling_params=dict(temperature=0.0),
+                         seeds=list(range(warm)), max_slots=per_gpu)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    mine, local, _ = generate_sharded(model, conds, max_new_tokens=n_new, sampling_params=dict(temperature=0.0),
+                                      seeds=list(range(n_utt)), gather=False, max_slots=per_gpu)
+    for c in local:
+        model.autoencoder.decode(c)
+    torch.cuda.synchronize()
+    busy = time.perf_counter() - t0
+    g0 = time.perf_counter()
+    gathered = None
+    if dist:
+        from zonos_vibes_amd.shard import gather_codes
+        gathered = gather_codes(local, mine, n_utt, 0, None, dev)
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gather_ms = (time.perf_counter() - g0) * 1e3
+    assert mine == mine_plan
+    frames = sum(int(c.shape[-1]) for c in local)
+    assert frames == sum(n_new[i] for i in mine)
+    stats = torch.tensor([wall, busy, frames], dtype=torch.float64, device=dev)
+    if dist:
+        allv = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(allv, stats)
+    else:
+        allv = [stats]
+    walls = [float(v[0]) for v in allv]
+    busys = [float(v[1]) for v in allv]
+    audio = sum(float(v[2]) for v in allv) * DAC_HOP / DAC_SAMPLE_RATE
+    res = {"config": f"C3: utterances 0..{n_utt - 1} of the 512-utterance C3 set (2-30 s, Lc 8 + 15 s, seed i), "
+                     f"LPT over {world} GPU(s), {per_gpu} slots per GPU, greedy, EOS suppressed, + DAC decode; "
+                     f"end-of-batch code gather to rank 0 ({'int16 over RCCL' if dist else 'none: one rank'})",
+           "utterances": n_utt, "audio_s": round(audio, 1), "rtf": round(audio / max(walls), 2),
+           "rtf_per_gpu": round(audio / max(walls) / world, 2),
+           "wall_s": round(max(walls), 3), "busy_s_per_rank": [round(b, 3) for b in busys],
+           "lpt_tail": round(max(busys) / (sum(busys) / len(busys)), 3), "gather_ms": round(gather_ms, 1)}
+    if rank == 0 and dist:
+        res["gathered_utterances"] = len(gathered)
+    return res
+
+
 def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430) -> dict:
     """One GPU's share of BASELINE config C5 (voice clone, long form): `slots` utterances of n_new frames
     (60 s) after a `prefix`-frame audio prompt (random codes), Lc = 160, greedy, EOS suppressed, through
@@ -335,11 +475,26 @@ def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430) -> dict:
 
 
 def cpu_cores() -> int:
-    """CPU threads available to this process: its affinity set, capped by OMP_NUM_THREADS when the host
-    sets one (the GPU box gives each GPU a 16-thread share and sets OMP_NUM_THREADS=16)."""
+    """CPU threads this process may use: its affinity set, capped by OMP_NUM_THREADS when the host sets one
+    (the GPU box gives each GPU process a 16-thread share of its host CPUs and sets OMP_NUM_THREADS=16)."""
     n = len(os.sched_getaffinity(0))
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return min(n, omp) if omp > 0 else n
+
+
+def cpu_info() -> dict:
+    """Host CPU model and counts, for the CPU-baseline line."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
@@ -386,7 +541,8 @@ def cpu_baseline(dev_weights: dict, cfg, budget_s: float = 20.0):
             "sample": f"C2 prefill (2x{LC + 1} rows) {t_pre:.2f}s + {n} decode steps at positions {p_lo}..{p_hi} "
                       f"(C2 mean {mean_pos}; {t_step * 1e3:.1f} ms/step, x{N_NEW + 8}) + DAC decode of {nf} of "
                       f"{N_NEW} frames ({t_dac * 1e3:.1f} ms/frame), extrapolated to the full utterance; "
-                      f"{threads} threads = this process's CPU share"}
+                      f"{threads} threads = this GPU process's share of the host CPUs (the box runs one GPU per "
+                      f"16-thread share and sets OMP_NUM_THREADS=16)", **cpu_info()}
 
 
 def _dac_weights_cpu():
@@ -427,23 +583,32 @@ def main():
         wav = model.autoencoder.decode(codes)
         return codes, wav
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):
         codes, wav = one_utterance()
     torch.cuda.synchronize()
+    ref_codes = codes.clone()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     frames = 0
+    timed_codes = []
     for _ in range(args.steps):
         codes, wav = one_utterance()
         frames += codes.shape[-1]
+        timed_codes.append(codes)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     assert codes.shape[-1] == n_new and wav.shape[-1] == n_new * DAC_HOP, (codes.shape, wav.shape)
+    # every timed utterance decoded exactly the warm-up's codes (greedy: a silent change fails the run)
+    for c in timed_codes:
+        if not torch.equal(c, ref_codes):
+            raise SystemExit("bench: a timed utterance's codes differ from the warm-up's (non-deterministic decode)")
+    import hashlib
+    codes_sha = hashlib.sha256(ref_codes.cpu().numpy().tobytes()).hexdigest()[:16]
     if dist:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -472,14 +637,17 @@ def main():
     # kernel-level measurement (outside the timed region)
     us, bl = time_dominant_kernel(model)
     step_us, step_pos = time_decode_step(model, cond)
+    ktab = kernel_table(model, cond)
     widened = time_widened_rows(model, dev)
     if rank == 0 and not args.no_hybrid:
         widened["hybrid_c4"] = time_hybrid(dev, n_new)
     if rank == 0 and not args.no_c5:
         widened["c5_share"] = time_c5(dev)
     breakdown = utterance_breakdown(model, cond, n_new)
-    if rank == 0 and not args.no_batch:
-        widened["batch_c3_sample"] = time_batch(model, dev)  # last: grows the engine to 64 slots
+    dac_tf = DAC_FLOP_PER_FRAME * n_new / (breakdown["dac_decode_ms"] * 1e-3) / 1e12
+    c3 = None
+    if not args.no_batch:
+        c3 = time_c3_sharded(model, dev, rank, world, dist)  # last: grows the engine to 64 slots
     out = None
     if rank == 0:
         achieved = bl / (us * 1e-6) / 1e9
@@ -504,7 +672,15 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": "profiles/r02g_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
+            "codes_sha256_16": codes_sha,
+            "c2_step_kernels": ktab,
             "utterance_breakdown": breakdown,
+            "dac_decode_roofline": {"bound": "mfma", "achieved": round(dac_tf, 1), "peak": MFMA_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": round(dac_tf / MFMA_PEAK_TFLOPS, 4),
+                                    "flop_per_frame": DAC_FLOP_PER_FRAME, "frames": n_new,
+                                    "ms": breakdown["dac_decode_ms"],
+                                    "mfma_busy_source": "profiles/r03_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
+            "c3_sharded": c3,
             "widened": widened,
             "end_of_batch_gather": gather,
         }

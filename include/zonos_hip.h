@@ -134,6 +134,16 @@ typedef struct ZmiPrefetch {
 } ZmiPrefetch;
 int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                       const ZmiPrefetch* prefetch, void* stream);
+/* Fused decode launch of a block's second half (reference _torch.py:100-101, 147-152 up to the SwiGLU):
+ * out_proj (EPI_RESIDUAL: X = the attention rows, out = the residual rows x, updated in place) and fc1
+ * (LayerNorm of the new x, packed SwiGLU weights [16384][2048], EPI_SWIGLU: out = h [M][8192]) in ONE
+ * launch of 256 workgroups (one per CU; needs 256 CUs): each streams its fc1 weight slice while the
+ * out_proj chain runs, and receives the new residual rows as {bf16 pair, tag = position + 1} granules
+ * (`gran`: zmi_ffn_block_gran_words(M) u64 words, out_proj->row_pos set; zero a row's words when it
+ * starts a new utterance). x and h are bit-identical to the two zmi_gemv_launch calls. 1 <= M <= 16;
+ * *err becomes nonzero if a wait gave up. */
+int zmi_ffn_block(const ZmiGemvArgs* out_proj, const ZmiGemvArgs* fc1, void* gran, unsigned* err, void* stream);
+int64_t zmi_ffn_block_gran_words(int rows);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);
@@ -317,6 +327,12 @@ int zmi_graph_destroy(void* graph_exec);
 
 const char* zmi_last_error(void);
 int zmi_version(void);
+/* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
+ *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the
+ *   dispatcher spreads their workgroups evenly over the CUs instead of packing several onto one CU. */
+enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_COUNT = 1 };
+int zmi_set_option(int which, int value);
+int zmi_get_option(int which);
 
 #ifdef __cplusplus
 }

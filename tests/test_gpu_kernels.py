@@ -90,6 +90,69 @@ def test_gemv_is_batch_invariant(K, ln):
         assert torch.equal(alt, ref)
 
 
+PROD_SHAPES = {  # Zonos-v0.1 decode GEMVs: (N, K, LayerNorm'd, epilogue, pack mode)
+    "qkv": (3072, 2048, True, "qkv", 0), "out_proj": (2048, 2048, False, "f32", 0),
+    "fc1": (16384, 2048, True, "swiglu", 1), "fc2": (2048, 8192, False, "f32", 0),
+    "heads": (9248, 2048, True, "f32", 0)}
+
+
+@pytest.mark.parametrize("name", list(PROD_SHAPES))
+def test_gemv_batch_invariant_production_shapes(name):
+    """The many-row GEMV geometries (4 column groups of 1024 threads, several row tiles per workgroup
+    with the next tile's rows DMA'd under the current one, per-shape workgroup targets) give every
+    row the bits of the decode-step launch (1-16 rows, single tile, LayerNorm prologue) at the
+    production shapes, epilogues included; the many-row plan LayerNorms its rows once per layer
+    (zmi_layernorm_rows), the decode plan in the GEMV prologue: generate_batch == generate rests
+    on exactly this."""
+    from zonos_vibes_amd.engine import rope_table
+    L = _lib()
+    N, K, ln, epi, mode = PROD_SHAPES[name]
+    big = 128
+    W = rnd(N, K, scale=0.03, seed=30)
+    X = rnd(big, K, scale=2.0, seed=31)
+    lnp = ((rnd(K, scale=0.1, seed=32) + 1).contiguous(), rnd(K, scale=0.02, seed=33)) if ln else None
+    packed = pack(W, mode)
+    rope = rope_table(128).to(DEV)
+    smax = 160
+    pos_all = torch.randint(0, smax, (big,), generator=torch.Generator().manual_seed(34), dtype=torch.int32).to(DEV)
+
+    def run(lo, hi, pre_ln):
+        m = hi - lo
+        xs = X[lo:hi].contiguous()
+        if pre_ln:  # the many-row plan: LayerNorm once, then the plain GEMV
+            xn = torch.zeros(m, K, dtype=torch.bfloat16, device=DEV)
+            L.check(L.lib().zmi_layernorm_rows(xs.data_ptr(), K, m, K, lnp[0].data_ptr(), lnp[1].data_ptr(), 1e-5,
+                                               xn.data_ptr(), K, stream_ptr()))
+            xs, use_ln = xn, None
+        else:
+            use_ln = lnp
+        if epi == "f32":
+            out = torch.zeros(m, N, dtype=torch.float32, device=DEV)
+            gemv(W, xs, L.EPI_F32, out, N, ln=use_ln, packed=packed)
+            return (out,)
+        if epi == "swiglu":
+            out = torch.zeros(m, N // 2, dtype=torch.bfloat16, device=DEV)
+            gemv(W, xs, L.EPI_SWIGLU, out, N // 2, ln=use_ln, packed=packed)
+            return (out,)
+        q = torch.zeros(m, 2048, dtype=torch.bfloat16, device=DEV)
+        kc = torch.zeros(m, 4, smax, 128, dtype=torch.bfloat16, device=DEV)
+        vt = torch.zeros(m, 4, 128, smax, dtype=torch.bfloat16, device=DEV)
+        row_kv = torch.arange(m, dtype=torch.int32, device=DEV)
+        row_pos = pos_all[lo:hi].contiguous()
+
+        def extra(a):
+            a.row_kv, a.row_pos, a.k_cache, a.v_cache = row_kv.data_ptr(), row_pos.data_ptr(), kc.data_ptr(), vt.data_ptr()
+            a.smax, a.hq, a.hkv, a.hd, a.rope = smax, 16, 4, 128, rope.data_ptr()
+        gemv(W, xs, L.EPI_QKV, q, 2048, ln=use_ln, packed=packed, extra=extra)
+        return q, kc, vt
+
+    ref = run(0, big, ln)
+    for lo, hi in [(0, 2), (0, 16), (6, 8), (5, 21), (100, 116), (126, 128), (16, 128), (0, 64)]:
+        got = run(lo, hi, ln and hi - lo > 4)
+        for r, g in zip(ref, got):
+            assert torch.equal(g, r[lo:hi]), (name, lo, hi)
+
+
 @pytest.mark.parametrize("K,M", [(2048, 2), (2048, 16), (2048, 37), (512, 5), (1024, 3)])
 def test_layernorm_rows_equals_gemv_prologue(K, M):
     """zmi_layernorm_rows (norm_f of the backbone plugin) and the GEMV LayerNorm prologue share one

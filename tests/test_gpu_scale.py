@@ -44,6 +44,51 @@ def test_generate_batch_many_slots_equals_single():
     assert torch.equal(again, single[5])
 
 
+def test_generate_batch_full_dims_64_slots_equals_single():
+    """C3 at the headline dims (Zonos-v0.1-transformer: 26 layers, d 2048, FFN 8192): 64 slots of short
+    mixed-length utterances run the production many-row GEMV shapes (N = 3072 / 16384 / 2048 / 9248 at
+    K = 2048 with 4 column groups, fc2 at K = 8192, several row tiles per workgroup, the LayerNorm
+    pre-pass) and the chunked attention kernel at 128 rows; 8 of the utterances, decoded alone by
+    generate() (2 rows: the fused decode block and the single-tile GEMVs), must give the same codes."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    n_utt, slots = 64, 64
+    lcs = [8 + (5 * i) % 23 for i in range(n_utt)]
+    lens = [6 + (11 * i) % 27 for i in range(n_utt)]
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_slots=slots, max_seqlen=max(lcs) + max(lens) + 16,
+                        max_prefill=max(lcs) + 8)
+    conds = [_cond(300 + i, lc, cfg.backbone.d_model).to(DEV) for i, lc in enumerate(lcs)]
+    params = dict(temperature=0.0)
+    batch = m.generate_batch(conds, max_new_tokens=lens, sampling_params=params, max_slots=slots)
+    m.engine.check_errors()
+    for i in (0, 5, 17, 23, 38, 41, 56, 63):
+        one = m.generate(conds[i], max_new_tokens=lens[i], sampling_params=params, progress_bar=False)
+        assert one.shape[-1] == lens[i]
+        assert torch.equal(one, batch[i]), i
+
+
+def test_attention_form_switch_keeps_codes():
+    """generate() whose positions cross the fused forms' reach (the chunk-split form to position 1023,
+    the score-exchange form to 1279, separate launches beyond): the engine switches graphs at those
+    positions inside one utterance, and the codes equal those of the separate launches throughout."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = transformer_config(2048, 2, 16, 4, 8192)
+    lc, n = 1000, 300  # positions 1001 .. 1308
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=lc + n + 16, max_prefill=lc + 8)
+    cond = _cond(77, lc, 2048).to(DEV)
+    params = dict(temperature=0.0)
+    e = m.engine
+    assert [f for f, _ in e._forms(2)][:2] == ["split", "xs"]
+    fused = m.generate(cond, max_new_tokens=n, sampling_params=params, progress_bar=False, chunk=128)
+    e.check_errors()
+    used = sorted({k[1] for k in e._graphs})
+    assert {"split", "xs", "none"} <= set(used), used
+    e.attn_block = False
+    e._build_plan()
+    plain = m.generate(cond, max_new_tokens=n, sampling_params=params, progress_bar=False, chunk=128)
+    assert torch.equal(fused, plain)
+
+
 def _ulp(x):
     return torch.ldexp(torch.ones_like(x), torch.frexp(x.abs().clamp_min(1e-30))[1] - 8)
 
@@ -138,7 +183,14 @@ def test_kv_capacity_8_slots_5784_positions():
         e.kc.normal_()
         e.vc.normal_()
     e.stream.synchronize()
+    e.pos_hi[:8] = [5760 + rows - 1] * 8  # host position bound (set by a prefill in generate())
     e.step(1, use_graph=True, slots=8)
     e.stream.synchronize()
     e.check_errors()
     assert torch.isfinite(e.logits[:rows]).all()
+    # the last layer's attention of three rows at ~5.77k keys against the blocking oracle and fp32 SDPA
+    from tests.test_gpu_kernels import _check_attention
+    last = cfg.backbone.n_layer - 1
+    pick = [0, 7, 15]
+    _check_attention(e.attn[pick], e.q[pick], e.kc[last][pick], e.vc[last][pick].transpose(-1, -2).contiguous(),
+                     [5760 + r for r in pick])

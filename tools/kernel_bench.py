@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--pos", type=int, default=591)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--attn-variants", default="0,1,4,8", help="zmi_attention_variant choices to time")
+    ap.add_argument("--spread", type=int, default=1, help="zmi_set_option(OPT_GEMV_SPREAD)")
     args = ap.parse_args()
+    _lib.check(_lib.lib().zmi_set_option(_lib.OPT_GEMV_SPREAD, args.spread))
     dev = torch.device("cuda", 0)
     cfg = zonos_v01_transformer()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=args.pos + 64, max_prefill=16,
@@ -42,6 +44,7 @@ def main():
         e.vc.normal_()
     e.stream.synchronize()
     e.attn_block = False  # the per-kernel breakdown of the unfused plan first
+    e.ffn_block = False
     plan = e._plan(rows)
     kinds = {"qkv": _lib.EPI_QKV, "swiglu(fc1)": _lib.EPI_SWIGLU, "logits(heads)": _lib.EPI_LOGITS}
     groups = {k: [it for kd, it in plan if kd == "gemv" and it[1] == epi] for k, epi in kinds.items()}
@@ -77,7 +80,7 @@ def main():
     e.attn_variant = variants[0]
     e.check_errors()
     for k, v in out.items():
-        print(json.dumps(dict(kernel=k, slots=args.slots, pos=args.pos, **v)), flush=True)
+        print(json.dumps(dict(kernel=k, slots=args.slots, pos=args.pos, spread=args.spread, **v)), flush=True)
     per_layer = sum(out[k]["us"] for k in ("qkv", "attention", "out_proj", "swiglu(fc1)", "fc2"))
     print(json.dumps(dict(kernel="sum_per_layer", us=round(per_layer, 2), step_estimate_us=round(
         per_layer * L + out["logits(heads)"]["us"], 1))), flush=True)

@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+from zonos_vibes_amd import _lib  # noqa: E402
 from zonos_vibes_amd.config import zonos_v01_transformer  # noqa: E402
 from zonos_vibes_amd.model import Zonos  # noqa: E402
 
@@ -35,7 +36,10 @@ def main():
     ref = None
     for opt in OPTIONS:
         for k, v in opt.items():
-            setattr(e, k, v)
+            if k.startswith("opt_"):  # library launch knobs: opt_gemv_spread -> zmi_set_option(OPT_GEMV_SPREAD)
+                _lib.check(e.lib.zmi_set_option(getattr(_lib, "OPT_" + k[4:].upper()), int(v)), k)
+            else:
+                setattr(e, k, v)
         e._build_plan()
         bench.time_decode_step(m, cond, steps=16)  # warm-up (graph capture)
         us, pos = bench.time_decode_step(m, cond)

@@ -17,6 +17,7 @@ c_int, c_int64, c_float, c_void_p, c_uint64 = ctypes.c_int, ctypes.c_int64, ctyp
 c_int_p = ctypes.POINTER(ctypes.c_int)
 
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
+OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
@@ -95,6 +96,8 @@ _SIGS = {
     "zmi_attn_block_max_pos": (c_int, [c_int]),
     "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
+    "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
+    "zmi_ffn_block_gran_words": (c_int64, [c_int]),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,
                                   ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
@@ -137,6 +140,8 @@ _SIGS = {
     "zmi_graph_destroy": (c_int, [c_void_p]),
     "zmi_last_error": (ctypes.c_char_p, []),
     "zmi_version": (c_int, []),
+    "zmi_set_option": (c_int, [c_int, c_int]),
+    "zmi_get_option": (c_int, [c_int]),
 }
 
 EXPORTED = sorted(_SIGS)

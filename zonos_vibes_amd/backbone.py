@@ -66,10 +66,14 @@ class HipZonosBackbone:
         lengths = inference_params.lengths_per_sample
         if lengths is None:
             lengths = torch.full((b,), inference_params.seqlen_offset, dtype=torch.int32, device=self.device)
-        max_pos = inference_params.seqlen_offset + s - 1
+        # K / V are written (and RoPE'd) at lengths_per_sample + arange(S) (_torch.py:74-77): bound those
+        l_max, l_min = (int(v) for v in torch.stack([lengths.max(), lengths.min()]).tolist())
+        max_pos = max(l_max, inference_params.seqlen_offset) + s - 1
+        if l_min < 0:
+            raise ValueError("negative lengths_per_sample")
         if max_pos >= e.smax:
             raise ValueError("positions beyond the allocated max_seqlen")
-        if e.hybrid and inference_params.seqlen_offset:
+        if e.hybrid and (inference_params.seqlen_offset or l_max):
             raise NotImplementedError("hybrid backbone plugin: prefill from position 0 only (decode runs inside "
                                       "generate(), whose step fuses the heads and sampler)")
         e.stream.wait_stream(torch.cuda.current_stream(self.device))

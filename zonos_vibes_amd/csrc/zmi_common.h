@@ -190,3 +190,5 @@ __device__ __forceinline__ bool zmi_last_arriver_wt(unsigned* counter, unsigned 
 
 int zmi_fail(hipError_t e, const char* what, const char* file, int line);
 int zmi_fail_msg(const char* msg);
+int zmi_option(int which);  // zmi_set_option knobs (zonos_hip.h ZMI_OPT_*)
+int zmi_cu_count();         // CUs of the current device (cached)

@@ -21,7 +21,7 @@
 //  * fixed reduction order, independent of M and of the tile a row lands in: per wave a
 //    chain of MFMAs over its k-segment (k-half 0 and k-half 1 in two accumulators), their sum,
 //    then the W segment sums in wave order.
-//  * optional LayerNorm prologue (nn.LayerNorm, _torch.py:62,88,90): one wave per row, fp32
+//  * optional LayerNorm prologue (nn.LayerNorm, _torch.py:62,88,90): (row, part) tasks over the waves, fp32
 //    two-pass statistics, bf16-rounded output, the same arithmetic for every row.
 //  * fused epilogues: bf16 store, residual add, RoPE + KV-cache write, SwiGLU, logits, raw f32.
 #pragma once
@@ -246,9 +246,11 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   // Each pass re-reads its chunks from LDS (no row copy in VGPRs: the weight slice in flight
   // already holds 4 NL of them, and occupancy decides whether every workgroup of a wide GEMV is
   // resident at once).
+#ifndef ZMI_LN_ROWWAVE  // (row, part) tasks spread over the waves, barriers between the passes; the A/B build
+                        // -DZMI_LN_ROWWAVE (one wave per row, no barriers) measured slower: C2 step 1001 vs 973 us
   if (PRO == PRO_LN) {
     constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
-    float* part = red;  // [RT][NQ] sums, then [RT][NQ] squared deviations at + RT NQ
+    float* part = red;
     const int ntask = rows * NQ;
     auto pass = [&](int task, float mean, bool sq) {
       const int r = task / NQ, q = task - r * NQ;
@@ -264,8 +266,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     }
     __syncthreads();
     for (int task = wave; task < ntask; task += NWV) {
-      const int r = task / NQ;
-      const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
+      const float mean = ln_combine<NQ>(part + (task / NQ) * NQ) / (float)K;
       const float v = pass(task, mean, true);
       if (lane == 0) part[RT * NQ + task] = v;
     }
@@ -285,6 +286,45 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     }
     __syncthreads();
   }
+#else
+  if (PRO == PRO_LN) {
+    // one wave per row: the row's NQ part sums (each the wave_sum of its lanes' chunk sums, as
+    // zmi_layernorm_rows forms them) are all held by that wave, so the three passes need no workgroup
+    // barrier; the row's own LDS writes and reads are ordered within the wave
+    constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
+    for (int r = wave; r < rows; r += NWV) {
+      bf16_t* xr = xs + r * XROW;
+      auto pass = [&](float mean, bool sq, float(&ps)[NQ]) {
+        float tq[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          tq[q] = 0.f;
+#pragma unroll
+          for (int i = 0; i < CPQ; ++i)
+            tq[q] += ln_chunk_sum(*reinterpret_cast<const uint4*>(xr + q * (K / NQ) + (lane + 64 * i) * 8), mean, sq);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) ps[q] = wave_sum(tq[q]);
+      };
+      float ps[NQ];
+      pass(0.f, false, ps);
+      const float mean = ln_combine<NQ>(ps) / (float)K;
+      pass(mean, true, ps);
+      const float rstd = 1.0f / sqrtf(ln_combine<NQ>(ps) / (float)K + a.eps), nbias = -mean * rstd;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < CPQ; ++i) {
+          const int c = q * (K / NQ) / 8 + lane + 64 * i;
+          bf16_t* xc = xr + q * (K / NQ) + (lane + 64 * i) * 8;
+          const uint4 xv = *reinterpret_cast<const uint4*>(xc);
+          *reinterpret_cast<uint4*>(xc) = ln_apply(xv, *reinterpret_cast<const uint4*>(gam + c * 8),
+                                                   *reinterpret_cast<const uint4*>(bet + c * 8), rstd, nbias);
+        }
+    }
+    __syncthreads();
+  }
+#endif
   if (PRO == PRO_ADDLN) {
     // layer_norm_fn prenorm: s = x + residual (fp32), LayerNorm(s) with (s - mean) rstd w + b; the column
     // block 0 workgroup of each row tile writes bf16(s), the next block's residual
@@ -599,16 +639,22 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
   auto fn = gemv_kernel<G, W, NL, RT, PRO, EPI, NTW>;
   const int n_cb = (a.N / 8 + G - 1) / G;
   const int n_rt = (a.M + RT - 1) / RT;
-  const size_t lds = Img<K>::bytes(a.M < RT ? a.M : RT, G * W, RT, PRO);
+  size_t lds = Img<K>::bytes(a.M < RT ? a.M : RT, G * W, RT, PRO);
   if (lds > LDS_MAX) return hipErrorInvalidValue;
+  const int rpw = rows_per_wg(n_cb, n_rt, K == 8192 ? 256 : 512);
+  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * ((n_rt + rpw - 1) / rpw);
+  if (NTW && zmi_option(ZMI_OPT_GEMV_SPREAD)) {
+    // a decode launch streams each weight once: its rate is the number of CUs it keeps busy (one CU
+    // pulls ~25 GB/s), so reserve LDS such that at most ceil(blocks / CUs) workgroups share a CU
+    const int64_t per_cu = (blocks + zmi_cu_count() - 1) / zmi_cu_count();
+    if (per_cu < 8) lds = std::max(lds, LDS_MAX / (size_t)(per_cu + 1) + 1024);
+  }
   if (lds > 64 * 1024) {
     static const hipError_t attr =  // once per instantiation: allow > 64 KiB of dynamic LDS
         hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
-  const int rpw = rows_per_wg(n_cb, n_rt, K == 8192 ? 256 : 512);
-  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * ((n_rt + rpw - 1) / rpw);
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt, rpw);
   return hipGetLastError();

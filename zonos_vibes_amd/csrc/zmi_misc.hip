@@ -18,7 +18,28 @@ int zmi_fail_msg(const char* msg) {
 }
 
 extern "C" const char* zmi_last_error(void) { return g_err; }
-extern "C" int zmi_version(void) { return 2; }
+extern "C" int zmi_version(void) { return 3; }
+
+// launch-geometry knobs (speed only: no option changes a result bit); defaults in the table
+static int g_opts[ZMI_OPT_COUNT] = {1};
+int zmi_option(int which) { return (which >= 0 && which < ZMI_OPT_COUNT) ? g_opts[which] : 0; }
+extern "C" int zmi_set_option(int which, int value) {
+  if (which < 0 || which >= ZMI_OPT_COUNT) return zmi_fail_msg("zmi_set_option: unknown option");
+  g_opts[which] = value;
+  return 0;
+}
+extern "C" int zmi_get_option(int which) { return zmi_option(which); }
+static int g_cus = 0;
+int zmi_cu_count() {
+  if (!g_cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_cus = n;
+    else
+      g_cus = 256;
+  }
+  return g_cus;
+}
 
 namespace {
 // Same stream as zonos_vibes_amd/synthetic.py: key + (i+1)*GOLDEN -> splitmix64 -> 24-bit uniform.

@@ -111,6 +111,9 @@ class HipEngine:
         self.prefetch_blocks = 192
         self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
+        # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= 16 rows at the v0.1 dims on a 256-CU device:
+        # fc1's weights stream while the out_proj chain runs (identical bits)
+        self.ffn_block = True
         self._plans: dict[tuple, list] = {}
         self._graphs: dict[tuple, int] = {}
         # host-side upper bound of each slot's next decode position (prefill sets it, every step adds 1):
@@ -148,7 +151,9 @@ class HipEngine:
             # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer; a row's
             # areas are zeroed when it starts an utterance (prefill), and its error word
             self.blk_gran = z(self.n_kv, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
-            self.blk_err = z(4, dt=torch.int32)
+            self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block
+            # zmi_ffn_block hand-off granules (the new residual rows), one area per layer
+            self.ffn_gran = z(self.L, R, self.lib.zmi_ffn_block_gran_words(1), dt=torch.int64)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -258,6 +263,10 @@ class HipEngine:
             return 8 | _lib.ATTNBLK_SPLIT
         return self.attn_self_slices | _lib.ATTNBLK_SELF if form == "self" else self.attn_block_slices
 
+    def _use_ffn_block(self, rows: int) -> bool:
+        return (self.ffn_block and rows <= 16 and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
+                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
+
     def _forms(self, rows: int) -> list:
         """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
         QKV and attention launches (any position)."""
@@ -328,10 +337,17 @@ class HipEngine:
                 else:
                     plan.append(("gemv", qkv))
                     plan.append(("attn", i))
-                plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)))
-                xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
-                plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
-                                                self.F, ln=ln)))
+                o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
+                if self._use_ffn_block(rows):
+                    o_item[0].row_pos = self.row_pos.data_ptr()
+                    f_item = self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
+                                        ln=(lw["ln2_w"], lw["ln2_b"]))
+                    plan.append(("ffnblk", (o_item[0], f_item[0], i)))
+                else:
+                    plan.append(("gemv", o_item))
+                    xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
+                    plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
+                                                    self.F, ln=ln)))
                 plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
             xin, ln = normed((w["nf_w"], w["nf_b"]))
             heads = self._gemv(w["heads"], xin, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
@@ -354,12 +370,30 @@ class HipEngine:
                                               self.attn.data_ptr(), self.H * self.hd, slices,
                                               ctypes.byref(pf), self.sptr), "attn_block")
 
+    def _run_ffn_block(self, item):
+        o, f, i = item
+        _lib.check(self.lib.zmi_ffn_block(ctypes.byref(o), ctypes.byref(f), self.ffn_gran[i].data_ptr(),
+                                          self.blk_err[3:].data_ptr(), self.sptr), "ffn_block")
+
     def check_errors(self):
-        """Raise if an attention launch gave up waiting on an in-launch hand-off (bounded spin)."""
-        if int(self.attn_work[:4].view(torch.int32).item()):
+        """Raise if a launch gave up waiting on an in-launch hand-off (bounded spin) or refused a row past
+        its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
+        attn = int(self.attn_work[:4].view(torch.int32).item())
+        blk, mamba, _, ffn = (int(v) for v in self.blk_err[:4].tolist())
+        if attn or blk or mamba or ffn:
+            self.attn_work[:4].zero_()
+            self.blk_err[:2].zero_()
+            self.blk_err[3:4].zero_()
+            self.stream.synchronize()
+        if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
-        if int(self.blk_err[0].item()):
-            raise RuntimeError("attn_block: a wait for the QKV projection timed out (results are invalid)")
+        if blk:
+            raise RuntimeError("attn_block: a hand-off wait timed out or a row was past the form's reach "
+                               "(results are invalid)")
+        if mamba:
+            raise RuntimeError("mamba_block: a wait for the in_proj output timed out (results are invalid)")
+        if ffn:
+            raise RuntimeError("ffn_block: a wait for the new residual rows timed out (results are invalid)")
 
     def refresh_inputs(self):
         """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
@@ -395,6 +429,8 @@ class HipEngine:
                 self._run_gemv(item)
             elif kind == "attnblk":
                 self._run_attn_block(item)
+            elif kind == "ffnblk":
+                self._run_ffn_block(item)
             elif kind == "attn":
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
                 self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
@@ -483,6 +519,7 @@ class HipEngine:
     def _reset_granules(self, slot: int):
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
         self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
+        self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
 
     def _prefill_logits(self, s_len: int):
         """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""

@@ -58,6 +58,27 @@ class HybridEngine(HipEngine):
         if (md["headdim"], md["d_state"], md["d_conv"], md["ngroups"]) != (64, 128, 4, 1) or not md["rmsnorm"] \
                 or md["norm_before_gate"] or md["D_has_hdim"]:
             raise NotImplementedError(f"Mamba2 geometry not built: {md}")
+        # MHA / Mamba2 options the kernels do not implement must not load silently (mamba_ssm MHA defaults:
+        # qkv_proj_bias / out_proj_bias True, causal False, rotary_emb_dim 0; Mamba2: dt_limit (0, inf))
+        ac, sc = dict(bb.attn_cfg), dict(bb.ssm_cfg)
+        hd = bb.d_model // int(ac.get("num_heads", 1))
+        bad = [k for k, ok in (
+            ("attn_cfg.rotary_emb_dim", int(ac.get("rotary_emb_dim", 0)) == hd),
+            ("attn_cfg.rotary_emb_interleaved", not ac.get("rotary_emb_interleaved", False)),
+            ("attn_cfg.rotary_emb_base", float(ac.get("rotary_emb_base", 10000.0)) == 10000.0),
+            ("attn_cfg.qkv_proj_bias", not ac.get("qkv_proj_bias", True)),
+            ("attn_cfg.out_proj_bias", not ac.get("out_proj_bias", True)),
+            ("attn_cfg.causal", bool(ac.get("causal", False))),
+            ("attn_cfg.softmax_scale", ac.get("softmax_scale") is None),
+            ("attn_cfg.d_conv", int(ac.get("d_conv", 0)) == 0),
+            ("attn_cfg.mlp_dim", int(ac.get("mlp_dim", 0)) == 0),
+            ("ssm_cfg.dt_limit", tuple(float(v) for v in sc.get("dt_limit", (0.0, float("inf")))) == (0.0, float("inf"))),
+            ("ssm_cfg.bias", not sc.get("bias", False)),
+            ("ssm_cfg.conv_bias", bool(sc.get("conv_bias", True))),
+            ("ssm_cfg.learnable_init_states", not sc.get("learnable_init_states", False)),
+        ) if not ok]
+        if bad:
+            raise NotImplementedError(f"hybrid options not built by the HIP kernels: {bad}")
         self.attn_idx = sorted(int(i) for i in bb.attn_layer_idx)
         self.Fm = int(bb.d_intermediate)
         super().__init__(cfg, device, max_slots, max_seqlen, max_prefill)
@@ -184,7 +205,7 @@ class HybridEngine(HipEngine):
         return run
 
     def _call_mamba_block(self, ia, sa, gran, out_w=None):
-        lib, s, ep, gp = self.lib, self.sptr, self.blk_err.data_ptr(), gran.data_ptr()
+        lib, s, ep, gp = self.lib, self.sptr, self.blk_err[1:].data_ptr(), gran.data_ptr()  # word 1: the Mamba2 block
         ia.row_pos = sa.row_pos  # the in_proj epilogue tags its granules with the row's position + 1
         pf = _lib.Prefetch()
         if out_w is not None and self.prefetch_blocks > 0:  # out_proj's weights into the Infinity Cache

@@ -51,6 +51,11 @@ class Zonos:
                   eos_row_scale: float | None = None, dac_seed: int = 0, **kw) -> "Zonos":
         m = cls(config, device, autoencoder=DACAutoencoder(device, seed=dac_seed), **kw)
         m.engine.init_synthetic(seed, zero_eos=zero_eos, eos_row_scale=eos_row_scale)
+        if m.prefix_conditioner is not None:
+            from . import synthetic as syn
+            pcc = config.prefix_conditioner
+            sd = dict(syn.iter_torch_cpu(syn.prefix_conditioner_specs(pcc.conditioners, config.backbone.d_model), seed))
+            m.prefix_conditioner.load_state_dict(sd, prefix="prefix_conditioner.")
         return m
 
     @classmethod

@@ -18,14 +18,26 @@ def sample_from_logits(logits: torch.Tensor, temperature: float = 1.0, top_p: fl
                        min_p: float = 0.0, linear: float = 0.0, conf: float = 0.0, quad: float = 0.0,
                        generated_tokens: torch.Tensor | None = None, repetition_penalty: float = 3.0,
                        repetition_penalty_window: int = 2, noise: torch.Tensor | None = None) -> torch.Tensor:
-    """logits [B, 9, 1026] -> tokens [B, 9, 1] int64 (device tensors)."""
-    if logits.dim() != 3 or logits.shape[1] != 9 or logits.shape[2] != 1026:
-        raise ValueError("logits must be [B, 9, 1026]")
+    """logits [B, 9, V] -> tokens [B, 9, 1] int64 (device tensors). V = 1025 (unpadded heads), 1026 (the
+    reference's padded heads) or wider (pad_vocab_to_multiple_of, model.py:37,46-51) with every column past
+    1025 at -inf, as _compute_logits leaves them (model.py:115): those never win, so they are dropped."""
+    if logits.dim() != 3 or logits.shape[1] != 9 or logits.shape[2] < 1025:
+        raise ValueError("logits must be [B, 9, V] with V >= 1025")
     dev = logits.device
     if dev.type != "cuda":
         raise ValueError("the HIP sampler takes device tensors")
-    b = logits.shape[0]
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    b, v = logits.shape[0], logits.shape[2]
+    if v == 1025:  # the kernel's row is 1026 wide: the missing column can never be drawn
+        logits = torch.cat([logits.float(), torch.full((b, 9, 1), float("-inf"), device=dev)], dim=-1)
+    elif v > 1026:
+        if not bool(torch.isneginf(logits[..., 1026:]).all()):
+            raise ValueError("logits past column 1025 must be -inf (the HIP sampler draws from 1026 columns)")
+        logits = logits[..., :1026]
+    if noise is not None and noise.shape[-1] != 1026:
+        noise = noise[..., :1026] if noise.shape[-1] > 1026 else torch.cat(
+            [noise.float(), torch.ones(b, 9, 1026 - noise.shape[-1], device=noise.device)], dim=-1)
+    # the reference draws its noise only when sampling (sampling.py:20-21); greedy leaves torch's RNG alone
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if temperature > 0 else 0
     prm = _lib.Sampling(float(temperature), float(top_p), float(min_p), float(linear), float(conf), float(quad),
                         float(repetition_penalty), 1.0, int(top_k), int(repetition_penalty_window), seed)
     p_dev = torch.tensor(bytearray(prm), dtype=torch.uint8).to(dev)

@@ -249,6 +249,34 @@ def dac_encoder_specs() -> list[Spec]:
     return out
 
 
+def prefix_conditioner_specs(conditioners: list[dict], d: int) -> list[Spec]:
+    """bf16 parameters of a PrefixConditioner (reference state-dict names under `prefix_conditioner.`,
+    conditioning.py:284-291), scaled like their module inits: embeddings and Fourier weights std 1,
+    linear projections uniform(+-1/sqrt(fan_in)), learned uncond vectors small and nonzero, LayerNorm
+    weight ~1."""
+    from .conditioning import PrefixConditioner
+    out = []
+    for name, shape in PrefixConditioner(conditioners, d, "cpu").param_shapes().items():
+        n = "prefix_conditioner." + name
+        if name == "norm.weight":
+            out.append(Spec(n, shape, "bf16", 0.1, 1.0))
+        elif name.endswith("project.weight"):
+            out.append(Spec(n, shape, "bf16", 1.0 / float(np.sqrt(shape[1]))))
+        elif name == "norm.bias" or name.endswith("project.bias"):
+            out.append(Spec(n, shape, "bf16", 0.02))
+        elif name.endswith("uncond_vector"):
+            out.append(Spec(n, shape, "bf16", 0.5))
+        else:  # phoneme / integer embedders, Fourier weights
+            out.append(Spec(n, shape, "bf16", SQRT3))
+    return out
+
+
+def synthetic_speaker_np(seed: int, dim: int = 128) -> np.ndarray:
+    """[1, dim] bf16 bits: a speaker embedding for the speaker conditioner (std 0.5)."""
+    key = tensor_key(seed, f"speaker/{dim}")
+    return f32_to_bf16_bits(uniform_f32(key, dim, 0.5 * SQRT3)).reshape(1, dim)
+
+
 def materialize_np(spec: Spec, seed: int = 0) -> np.ndarray:
     """numpy array for `spec` (bf16 returned as uint16 bit patterns)."""
     key = tensor_key(seed, spec.name)
