@@ -41,43 +41,61 @@ def cond_tensor(seed: int, d: int, dev, lc: int = LC):
 
 
 def time_dominant_kernel(model, reps: int = 3):
-    """fc1 GEMV (+LN prologue, SwiGLU epilogue) of every layer, timed with HIP events on the engine stream.
-
-    Rotating over all 26 layers' 67 MB weights (1.7 GB) keeps the stream out of the 256 MiB
-    Infinity Cache, so the bytes come from HBM as in the decode step.
-    """
+    """The largest kernel of the C2 step, zmi_ffn_block (out_proj + residual, LayerNorm, fc1, SwiGLU: 75.5 MB
+    of weights per launch), for every layer, timed with HIP events on the engine stream one launch at a
+    time with its hand-off granules zeroed first (a re-run at the same position would find its own
+    granules). Rotating over all 26 layers' weights (2 GB) keeps the stream out of the 256 MiB Infinity
+    Cache, so the bytes come from HBM as in the decode step. Returns (us per launch, algorithmic bytes)."""
     e = model.engine
-    items = [item for kind, item in e._plan(2) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
-    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    items = [item for kind, item in e._plan(2) if kind == "ffnblk"]
+    assert items, "the C2 plan has no fused out_proj + fc1 launch"
     with torch.cuda.stream(e.stream):
-        for it in items:
-            e._run_gemv(it)
-        start.record(e.stream)
-        for _ in range(reps):
-            for it in items:
-                e._run_gemv(it)
-        end.record(e.stream)
-    end.synchronize()
-    n = reps * len(items)
-    us = start.elapsed_time(end) * 1000.0 / n
-    bytes_launch = 2 * e.F * e.d * 2 + 2 * e.d * 2 + 2 * e.F * 2 + 2 * e.d * 2
+        e.row_pos[:2] = 591
+    us = _time_fused(e, items, e.ffn_gran, e._run_ffn_block, reps)
+    with torch.cuda.stream(e.stream):
+        e.row_pos[:2] = -1
+    e.check_errors()
+    d, F = e.d, e.F
+    bytes_launch = (d * d + 2 * F * d) * 2 + 2 * d * 2 * 3 + 2 * d * 2 + 2 * F * 2  # weights, attn/x in, x out, ln, h out
     return us, bytes_launch
 
 
-FC1_KERNEL = "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"  # G, W, NL, RT, PRO_LN, EPI_SWIGLU, non-temporal
+DOMINANT_KERNEL = "ffn_block_kernel"
+
+
+def _time_fused(e, items, gran, run, reps: int) -> float:
+    """us per launch of a fused launch kind (hand-off granules per layer): the 26 layers' launches back to
+    back on the engine stream, each layer's granule area zeroed before the run (outside the events), so
+    every launch waits for its own producers as in the decode step."""
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tot = 0.0
+    with torch.cuda.stream(e.stream):
+        for r in range(reps + 1):
+            gran.zero_()
+            st.record(e.stream)
+            for it in items:
+                run(it)
+            en.record(e.stream)
+            en.synchronize()
+            if r:
+                tot += st.elapsed_time(en) * 1000.0
+    return tot / (reps * len(items))
+
+
+PMC_FILE = "r03_pmc_ffnblk_fetch.json"
 
 
 def pmc_traffic():
-    """HBM bytes per fc1 launch from the committed FETCH_SIZE pass of THIS kernel (tools/prof_round.sh:
-    rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950 correction; a counter pass
-    serialises dispatches, so it is not repeated inside the timed run). None when the profile is
-    absent or measured another kernel."""
-    path = os.path.join(REPO, "profiles", "r02g_pmc_fc1_fetch.json")
+    """HBM bytes per launch of the dominant kernel from the committed FETCH_SIZE pass of THIS kernel
+    (tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py ffnblk, x2 gfx950
+    correction; a counter pass serialises dispatches, so it is not repeated inside the timed run). None
+    when the profile is absent or measured another kernel."""
+    path = os.path.join(REPO, "profiles", PMC_FILE)
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    if not d.get("kernels") or any(FC1_KERNEL not in k for k in d["kernels"]):
+    if not d.get("kernels") or any(DOMINANT_KERNEL not in k for k in d["kernels"]):
         return None
     return int(d["FETCH_SIZE_bytes_per_launch"])
 
@@ -107,10 +125,11 @@ def time_decode_step(model, cond, steps: int = 64):
 
 def kernel_table(model, cond, reps: int = 3) -> dict:
     """Every kernel of the C2 decode step at the utterance's mean position, timed on the engine stream
-    with HIP events: the GEMVs as all 26 layers' launches back to back (each weight from HBM, as in the
-    step), the fused QKV + attention launch one launch at a time with its hand-off granules zeroed first
-    (a re-run at the same position would otherwise find its own granules and skip the wait), the sampler
-    alone. Per kernel: avg us per launch, algorithmic bytes per launch, GB/s and fraction of HBM peak."""
+    with HIP events, each kind as all 26 layers' launches back to back (each weight from HBM, as in the
+    step; a launch's time includes its boundary with the previous one); the fused launches with every
+    layer's hand-off granules zeroed before the run (a re-run at the same position would otherwise find
+    its own granules and skip the wait); heads and sampler as repeated single launches. Per kernel: avg
+    us per launch, algorithmic bytes per launch, GB/s and fraction of HBM peak."""
     from zonos_vibes_amd.engine import SamplingParams
     e = model.engine
     s_len = e.prefill(0, cond, None, N_NEW, SamplingParams(temperature=0.0, cfg_scale=2.0))
@@ -122,12 +141,15 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     d, F, qkv_n = e.d, e.F, (e.H + 2 * e.Hkv) * e.hd
     kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)  # K + V of both CFG rows, one layer
     gem = [it for kd, it in plan if kd == "gemv"]
+    res = [it for it in gem if it[1] == _lib.EPI_RESIDUAL]
+    fused_ffn = any(kd == "ffnblk" for kd, _ in plan)
     kinds = {
-        "out_proj": ([it for it in gem if it[1] == _lib.EPI_RESIDUAL][0::2], d * d * 2),
+        "out_proj": ([] if fused_ffn else res[0::2], d * d * 2),
         "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2),
-        "fc2": ([it for it in gem if it[1] == _lib.EPI_RESIDUAL][1::2], d * F * 2),
+        "fc2": (res if fused_ffn else res[1::2], d * F * 2),
         "heads (LN + logits)": ([it for it in gem if it[1] == _lib.EPI_LOGITS], 9 * 1025 * d * 2),
     }
+    kinds = {k: v for k, v in kinds.items() if v[0]}
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {}
     with torch.cuda.stream(e.stream):
@@ -143,18 +165,16 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
             us = st.elapsed_time(en) * 1000.0 / (reps * len(items))
             out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
                              hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items))
+        ffn = [it for kd, it in plan if kd == "ffnblk"]
+        if ffn:
+            us = _time_fused(e, ffn, e.ffn_gran, e._run_ffn_block, reps)
+            nbytes = (d * d + 2 * F * d) * 2
+            out["ffn_block (out_proj + residual + LN + fc1 + SwiGLU)"] = dict(
+                us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
+                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(ffn))
         blk = [it for kd, it in plan if kd == "attnblk"]
         if blk:
-            tot = 0.0
-            for _ in range(reps):
-                for it in blk:
-                    e.blk_gran[it[1]].zero_()
-                    st.record(e.stream)
-                    e._run_attn_block(it)
-                    en.record(e.stream)
-                    en.synchronize()
-                    tot += st.elapsed_time(en) * 1000.0
-            us = tot / (reps * len(blk))
+            us = _time_fused(e, blk, e.blk_gran, e._run_attn_block, reps)
             nbytes = qkv_n * d * 2 + kv
             out[f"attn_block ({form}: LN + QKV + RoPE + KV write + attention)"] = dict(
                 us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
@@ -667,10 +687,11 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv_kernel<G=2,W=4,NL=8,RT=16,LN,SWIGLU> (fc1, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": "ffn_block_kernel (out_proj + residual + LayerNorm + fc1 + SwiGLU, 75.5 MB bf16 "
+                                   "weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
-                         "traffic_source": "profiles/r02g_pmc_fc1_fetch.json (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "codes_sha256_16": codes_sha,
             "c2_step_kernels": ktab,

@@ -6,6 +6,7 @@ C2 mean position, on the synthetic Zonos-v0.1 engine (B = 1, two CFG rows).
         python tools/pmc_driver.py fc1
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attn        (and WRITE_SIZE)
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention)
+    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py ffnblk      (fused out_proj + fc1)
 then tools/pmc_summary.py turns the counter CSV into the per-launch JSON kept under profiles/.
 """
 import os
@@ -33,6 +34,9 @@ def main(which: str, reps: int = 2):
         e.vc.normal_()
     e.stream.synchronize()
     e.pos_hi[0] = POS
+    if which == "fc1":  # the standalone fc1 GEMV (the C2 step runs it inside zmi_ffn_block)
+        e.ffn_block = False
+        e._build_plan()
     plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
     for _ in range(reps):
         if which == "fc1":
@@ -42,6 +46,11 @@ def main(which: str, reps: int = 2):
         elif which == "attn":
             for i in range(e.L):
                 e._attention(i, e.q, 2, None, e.row_pos, e.smax - 1, e.attn)
+        elif which == "ffnblk":  # the fused out_proj + fc1 launch of every layer (granules fresh per launch)
+            for kind, it in plan:
+                if kind == "ffnblk":
+                    e.ffn_gran[it[2]].zero_()
+                    e._run_ffn_block(it)
         elif which == "attnblk":  # the fused QKV + attention launch of every layer (granules fresh per rep)
             e.blk_gran.zero_()
             for kind, it in plan:
