@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--attn-variants", default="0,1,4,8", help="zmi_attention_variant choices to time")
     ap.add_argument("--spread", type=int, default=1, help="zmi_set_option(OPT_GEMV_SPREAD)")
+    ap.add_argument("--gemm-rows", default="1", help="zmi_set_option(OPT_GEMM_ROWS) values to time the GEMVs under")
     args = ap.parse_args()
     _lib.check(_lib.lib().zmi_set_option(_lib.OPT_GEMV_SPREAD, args.spread))
     dev = torch.device("cuda", 0)
@@ -66,10 +67,16 @@ def main():
         return st.elapsed_time(en) * 1000.0 / (args.reps * n)
 
     out = {}
-    for name, items in groups.items():
-        us = timed(lambda: [e._run_gemv(it) for it in items], len(items))
-        gbs = wbytes[name] / (us * 1e-6) / 1e9
-        out[name] = dict(us=round(us, 2), weight_bytes=wbytes[name], GBps=round(gbs, 1), hbm_frac=round(gbs / 8000, 3))
+    rows_opts = [int(v) for v in args.gemm_rows.split(",")]
+    for ro in rows_opts:
+        _lib.check(_lib.lib().zmi_set_option(_lib.OPT_GEMM_ROWS, ro))
+        for name, items in groups.items():
+            us = timed(lambda: [e._run_gemv(it) for it in items], len(items))
+            gbs = wbytes[name] / (us * 1e-6) / 1e9
+            key = name if ro == rows_opts[0] else f"{name}_rows{ro}"
+            out[key] = dict(us=round(us, 2), weight_bytes=wbytes[name], GBps=round(gbs, 1),
+                            hbm_frac=round(gbs / 8000, 3), gemm_rows=ro)
+    _lib.check(_lib.lib().zmi_set_option(_lib.OPT_GEMM_ROWS, rows_opts[0]))
     kv = rows * e.Hkv * e.hd * 2 * 2 * (args.pos + 1)
     variants = [int(v) for v in args.attn_variants.split(",")]
     for var in variants:

@@ -18,6 +18,7 @@ c_int_p = ctypes.POINTER(ctypes.c_int)
 
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
 OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
+OPT_GEMM_ROWS = 1
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3

@@ -122,6 +122,104 @@ struct QkvFuse {
   int gran_stride;
 };
 
+// (6) fused epilogues of one group's 8 columns over a row tile, run by one wave; colsum(c, r) = the
+// group's finished column sum. Shared by every launch form (gemv_body, gemm_rows_kernel): the same bits.
+template <int EPI, int RT, int FUSE, class ColSum>
+__device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& colsum, int lane, int rows, int row0,
+                                         int g, const uint32_t (&res_pre)[(8 * RT + 63) / 64], int q_pos, int q_kvr,
+                                         const QkvFuse& fz) {
+  constexpr int NE = (8 * RT + 63) / 64;
+  const int col0 = g * 8;
+  if (EPI == ZMI_EPI_STORE && FUSE == 2) {
+    // plain bf16 store, and every column pair of an active row also goes out as an 8-byte {pair,
+    // tag = position + 1} granule (zmi_mamba_block's step role reads the in_proj output from these)
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
+      const bool ok = r < rows && n < a.n_valid;
+      const uint32_t hv = ok ? f2bf(colsum(c, r)) : 0u;
+      const uint32_t nb = (uint32_t)__shfl_down((int)hv, 1);
+      if (ok) {
+        const size_t m = (size_t)(row0 + r);
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)hv;
+        const int pos = a.row_pos[m];
+        if ((c & 1) == 0 && pos >= 0)
+          st_wt64(fz.gran + m * fz.gran_stride + (n >> 1), (uint64_t)(hv | (nb << 16)) | ((uint64_t)(unsigned)(pos + 1) << 32));
+      }
+    }
+  } else if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
+      if (r >= rows || n >= a.n_valid) continue;
+      const float v = colsum(c, r);
+      const size_t m = (size_t)(row0 + r);
+      if (EPI == ZMI_EPI_F32) {
+        reinterpret_cast<float*>(a.out)[m * a.ldo + n] = v;
+      } else if (EPI == ZMI_EPI_STORE) {
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(v);
+      } else if (EPI == ZMI_EPI_RESIDUAL) {
+        // x + bf16(linear(x))  (_torch.py:100-101)
+        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(bf2f(res_pre[i]) + bfround(v));
+      } else {
+        // 9 heads back to back, 1026 columns each (1025 real + the zero pad row)
+        const int cbk = n / 1026, vv = n - cbk * 1026;
+        reinterpret_cast<float*>(a.out)[(m * 9 + cbk) * 1026 + vv] = bfround(v);
+      }
+    }
+  } else if (EPI == ZMI_EPI_SWIGLU) {
+    // M8 SwiGLU packing: columns 0..3 = value rows 4g.., 4..7 = gate rows F + 4g..  (_torch.py:150-152)
+    const int r = lane >> 2, c = lane & 3;
+    if (r < rows) {
+      const float y = bfround(colsum(c, r));
+      const float gt = bfround(colsum(c + 4, r));
+      const float sg = bfround(gt / (1.0f + expf(-gt)));
+      reinterpret_cast<bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + g * 4 + c] = (bf16_t)f2bf(y * sg);
+    }
+  } else if (EPI == ZMI_EPI_QKV) {
+    // q | k | v split, interleaved-pair RoPE in fp32 on q and k, KV-cache write (_torch.py:18-49,117-126)
+    const int r = lane >> 2, c = (lane & 3) * 2;
+    if (r < rows && q_pos >= 0 && q_pos < a.smax) {  // the launchers check positions against smax; never write past it
+      const int n = col0 + c;
+      const int qcols = a.hq * a.hd, kcols = a.hkv * a.hd;
+      float x0 = bfround(colsum(c, r)), x1 = bfround(colsum(c + 1, r));
+      if (n < qcols + kcols) {
+        const int d = (n < qcols ? n : n - qcols) % a.hd;
+        const float2 cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
+        const float co = cs.x, si = cs.y;
+        const float r0 = x0 * co - x1 * si;
+        const float r1 = x1 * co + x0 * si;
+        x0 = r0;
+        x1 = r1;
+      }
+      const uint32_t packed = f2bf(x0) | (f2bf(x1) << 16);
+      int gkh = 0, gslot = 0;  // granule of this pair (FUSE)
+      if (n < qcols) {
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)(row0 + r) * a.ldo + n) = packed;
+        const int gq = a.hq / a.hkv;
+        gkh = n / (gq * a.hd);
+        gslot = (n - gkh * gq * a.hd) >> 1;
+      } else if (n < qcols + kcols) {  // K cache [row][kv head][position][hd]
+        const int nn = n - qcols, kh = nn / a.hd, d = nn - kh * a.hd;
+        const size_t o = (((size_t)q_kvr * a.hkv + kh) * a.smax + q_pos) * a.hd + d;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.k_cache) + o) = packed;
+        gkh = kh;
+        gslot = (a.hq / a.hkv) * (a.hd >> 1) + (d >> 1);
+      } else {  // V cache, transposed: [row][kv head][hd][position] (zmi_attn.hip's P.V operand)
+        const int nn = n - qcols - kcols, kh = nn / a.hd, d = nn - kh * a.hd;
+        bf16_t* vt = reinterpret_cast<bf16_t*>(a.v_cache) + (((size_t)q_kvr * a.hkv + kh) * a.hd + d) * a.smax + q_pos;
+        vt[0] = (bf16_t)(packed & 0xffffu);
+        vt[a.smax] = (bf16_t)(packed >> 16);
+        gkh = kh;
+        gslot = (a.hq / a.hkv + 1) * (a.hd >> 1) + (d >> 1);
+      }
+      if (FUSE)
+        st_wt64(fz.gran + ((size_t)(row0 + r) * a.hkv + gkh) * fz.gran_stride + gslot,
+                (uint64_t)packed | ((uint64_t)(unsigned)(q_pos + 1) << 32));
+    }
+  }
+}
+
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW, int FUSE = 0>
 __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_rt, int b, char* smem,
                                           const QkvFuse& fz, int rpw = 1) {
@@ -472,103 +570,14 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     stage_rows(false, n_row0, min(RT, a.M - n_row0), reinterpret_cast<const bf16_t*>(a.X) + (size_t)n_row0 * a.ldx);
   }
   if (ew) {
-  auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
-    float v = red[((gi * W) * 8 + c) * RT + r];
+    auto colsum = [&](int c, int r) {  // the group's W segment sums, in wave order
+      float v = red[((gi * W) * 8 + c) * RT + r];
 #pragma unroll
-    for (int w = 1; w < W; ++w) v += red[((gi * W + w) * 8 + c) * RT + r];
-    return v;
-  };
-
-  // (6) fused epilogues
-  if (EPI == ZMI_EPI_STORE && FUSE == 2) {
-    // plain bf16 store, and every column pair of an active row also goes out as an 8-byte {pair,
-    // tag = position + 1} granule (zmi_mamba_block's step role reads the in_proj output from these)
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
-      const bool ok = r < rows && n < a.n_valid;
-      const uint32_t hv = ok ? f2bf(colsum(c, r)) : 0u;
-      const uint32_t nb = (uint32_t)__shfl_down((int)hv, 1);
-      if (ok) {
-        const size_t m = (size_t)(row0 + r);
-        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)hv;
-        const int pos = a.row_pos[m];
-        if ((c & 1) == 0 && pos >= 0)
-          st_wt64(fz.gran + m * fz.gran_stride + (n >> 1), (uint64_t)(hv | (nb << 16)) | ((uint64_t)(unsigned)(pos + 1) << 32));
-      }
-    }
-  } else if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
-      if (r >= rows || n >= a.n_valid) continue;
-      const float v = colsum(c, r);
-      const size_t m = (size_t)(row0 + r);
-      if (EPI == ZMI_EPI_F32) {
-        reinterpret_cast<float*>(a.out)[m * a.ldo + n] = v;
-      } else if (EPI == ZMI_EPI_STORE) {
-        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(v);
-      } else if (EPI == ZMI_EPI_RESIDUAL) {
-        // x + bf16(linear(x))  (_torch.py:100-101)
-        reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)f2bf(bf2f(res_pre[i]) + bfround(v));
-      } else {
-        // 9 heads back to back, 1026 columns each (1025 real + the zero pad row)
-        const int cbk = n / 1026, vv = n - cbk * 1026;
-        reinterpret_cast<float*>(a.out)[(m * 9 + cbk) * 1026 + vv] = bfround(v);
-      }
-    }
-  } else if (EPI == ZMI_EPI_SWIGLU) {
-    // M8 SwiGLU packing: columns 0..3 = value rows 4g.., 4..7 = gate rows F + 4g..  (_torch.py:150-152)
-    const int r = lane >> 2, c = lane & 3;
-    if (r < rows) {
-      const float y = bfround(colsum(c, r));
-      const float gt = bfround(colsum(c + 4, r));
-      const float sg = bfround(gt / (1.0f + expf(-gt)));
-      reinterpret_cast<bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + g * 4 + c] = (bf16_t)f2bf(y * sg);
-    }
-  } else if (EPI == ZMI_EPI_QKV) {
-    // q | k | v split, interleaved-pair RoPE in fp32 on q and k, KV-cache write (_torch.py:18-49,117-126)
-    const int r = lane >> 2, c = (lane & 3) * 2;
-    if (r < rows && q_pos >= 0 && q_pos < a.smax) {  // the launchers check positions against smax; never write past it
-      const int n = col0 + c;
-      const int qcols = a.hq * a.hd, kcols = a.hkv * a.hd;
-      float x0 = bfround(colsum(c, r)), x1 = bfround(colsum(c + 1, r));
-      if (n < qcols + kcols) {
-        const int d = (n < qcols ? n : n - qcols) % a.hd;
-        const float2 cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
-        const float co = cs.x, si = cs.y;
-        const float r0 = x0 * co - x1 * si;
-        const float r1 = x1 * co + x0 * si;
-        x0 = r0;
-        x1 = r1;
-      }
-      const uint32_t packed = f2bf(x0) | (f2bf(x1) << 16);
-      int gkh = 0, gslot = 0;  // granule of this pair (FUSE)
-      if (n < qcols) {
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.out) + (size_t)(row0 + r) * a.ldo + n) = packed;
-        const int gq = a.hq / a.hkv;
-        gkh = n / (gq * a.hd);
-        gslot = (n - gkh * gq * a.hd) >> 1;
-      } else if (n < qcols + kcols) {  // K cache [row][kv head][position][hd]
-        const int nn = n - qcols, kh = nn / a.hd, d = nn - kh * a.hd;
-        const size_t o = (((size_t)q_kvr * a.hkv + kh) * a.smax + q_pos) * a.hd + d;
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(a.k_cache) + o) = packed;
-        gkh = kh;
-        gslot = (a.hq / a.hkv) * (a.hd >> 1) + (d >> 1);
-      } else {  // V cache, transposed: [row][kv head][hd][position] (zmi_attn.hip's P.V operand)
-        const int nn = n - qcols - kcols, kh = nn / a.hd, d = nn - kh * a.hd;
-        bf16_t* vt = reinterpret_cast<bf16_t*>(a.v_cache) + (((size_t)q_kvr * a.hkv + kh) * a.hd + d) * a.smax + q_pos;
-        vt[0] = (bf16_t)(packed & 0xffffu);
-        vt[a.smax] = (bf16_t)(packed >> 16);
-        gkh = kh;
-        gslot = (a.hq / a.hkv + 1) * (a.hd >> 1) + (d >> 1);
-      }
-      if (FUSE)
-        st_wt64(fz.gran + ((size_t)(row0 + r) * a.hkv + gkh) * fz.gran_stride + gslot,
-                (uint64_t)packed | ((uint64_t)(unsigned)(q_pos + 1) << 32));
-    }
+      for (int w = 1; w < W; ++w) v += red[((gi * W + w) * 8 + c) * RT + r];
+      return v;
+    };
+    epilogue<EPI, RT, FUSE>(a, colsum, lane, rows, row0, g, res_pre, q_pos, q_kvr, fz);  // (6)
   }
-  }  // ew
   ZMI_GSTAMP(6);
   // one tile when each weight is read once (NTW: M <= RT, every decode launch): no loop state there
   if (NTW || ++rt >= rt_end) break;
@@ -586,6 +595,180 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
   extern __shared__ __attribute__((aligned(16))) char smem[];
   gemv_body<G, W, NL, RT, PRO, EPI, NTW>(a, n_cb, n_rt, blockIdx.x, smem, QkvFuse{nullptr, 0}, rpw);
 }
+
+// s_waitcnt vmcnt(n) as the builtin (gfx9 encoding, expcnt / lgkmcnt left at their maxima): unlike an asm
+// wait, the compiler's own wait insertion sees it, so loads it covers are not waited for again after
+// later (uncounted) LDS-DMA issues
+#define ZMI_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70)
+
+// Many-row form of the K = 2048 GEMV (multi-slot decode and prefill, M > 16), the same per-row arithmetic as
+// gemv_body's (W, NL, RT) = (4, 8, 16) shape: a wave's chain of MFMAs over one k-segment (k-half 0 / 1 in
+// two accumulators, acc0 + ror8(acc1)), then the 4 segment sums in segment order, then epilogue().
+// What changes is the reuse: a workgroup owns 8 groups (64 columns) and each wave GPW of them over one
+// segment (GPW x 32 weight VGPRs), so every activation tile it stages serves 64 columns (gemv_body's 4-group
+// form: 32, twice the activation traffic per column) and each A fragment read from LDS feeds GPW groups; the
+// activation tiles are double-buffered, the next tile's DMA issued as the current tile's chains start.
+// Group gi's epilogue runs on wave gi (the first 8 waves: two or one per SIMD). One workgroup per CU.
+constexpr int GR_G = 8, GR_RT = 16, GR_XROW = 2048 + 8;
+constexpr size_t GR_RED = (size_t)2 * GR_RT * GR_XROW * 2;
+constexpr size_t GR_LDS = GR_RED + (size_t)GR_G * 4 * 8 * GR_RT * 4;
+
+template <int EPI, int GPW>
+__global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const ZmiGemvArgs a, int n_cb, int n_rt,
+                                                                        int rpw) {
+  constexpr int W = 4, NL = 8, RT = GR_RT, K = 2048, KC = K / 64, XROW = GR_XROW, NE = 2;
+  constexpr int NGS = GR_G / GPW, NWV = NGS * W, PPW = RT * (K / 512) / NWV;  // group sets, waves, DMA pieces / wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);                 // [2][RT][XROW] activation tiles
+  float* red = reinterpret_cast<float*>(smem + GR_RED);          // [group][segment][8][RT] segment sums
+  const int b = blockIdx.x, idx = b >> 3;
+  const int n_rg = (n_rt + rpw - 1) / rpw;
+  const int cb = (idx / n_rg) * 8 + (b & 7), rg = idx - (idx / n_rg) * n_rg;  // gemv_body's XCD-aware map
+  if (cb >= n_cb) return;
+  ZMI_GSTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gs = wave % NGS, wk = wave / NGS;  // groups gs + NGS h (h < GPW) over segment wk
+  const int ngroups = a.N >> 3;
+  int gg[GPW];
+#pragma unroll
+  for (int h = 0; h < GPW; ++h) gg[h] = min(cb * GR_G + gs + NGS * h, ngroups - 1);  // clamped: discarded
+  // the epilogue of group eg = wave (waves 0..7)
+  const bool ew = wave < GR_G && cb * GR_G + wave < ngroups;
+  const int eg = cb * GR_G + wave;
+  int rt = rg * rpw;
+  const int rt_end = min(n_rt, rt + rpw);
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X);
+
+  // a tile = 16 rows x 4 KiB = 64 DMA pieces, PPW per wave (rows past M re-read row M - 1: their outputs are
+  // discarded, and every wave issues the same count, which the vmcnt waits below rely on)
+  auto dma_tile = [&](int t) {
+    bf16_t* dst = xs + (t & 1) * RT * XROW;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = wave + NWV * i, r = pc >> 2, p = pc & 3;
+      const int sr = min(t * RT + r, a.M - 1);
+      dma_piece(X + (size_t)sr * a.ldx + p * 512 + lane * 8, dst + r * XROW + p * 512);
+    }
+  };
+  // epilogue operands of tile t (epilogue waves): the group's residual inputs, the row's position / cache row
+  auto load_epi = [&](int t, uint32_t(&res)[NE], int& qp, int& qk) {
+    const int row0 = t * RT, rows = min(RT, a.M - row0);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) res[i] = 0;
+    qp = -1;
+    qk = 0;
+    if (!ew) return;
+    if (EPI == ZMI_EPI_RESIDUAL) {
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = lane + 64 * i, r = e >> 3, n = eg * 8 + (e & 7);
+        if (r < rows && n < a.n_valid) res[i] = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + n];
+      }
+    }
+    if (EPI == ZMI_EPI_QKV && (lane >> 2) < rows) {
+      qp = a.row_pos[row0 + (lane >> 2)];
+      qk = a.row_kv[row0 + (lane >> 2)];
+    }
+  };
+
+  uint32_t res_cur[NE], res_nxt[NE];
+  int qp_cur, qk_cur, qp_nxt = -1, qk_nxt = 0;
+  dma_tile(rt);
+  load_epi(rt, res_cur, qp_cur, qk_cur);
+  __builtin_amdgcn_sched_barrier(0);
+  // the weight slices of the wave's groups (GPW NL x 16 B per lane), in flight at once, in chain order (chunk
+  // j of every group before chunk j + 1): the first tile's chains follow them as they land. Re-read by the
+  // other row groups of this column block from L2 (temporal).
+  u32x4_t wf[GPW][NL];
+  {
+    __amdgpu_buffer_rsrc_t wrsrc[GPW];
+#pragma unroll
+    for (int h = 0; h < GPW; ++h)
+      wrsrc[h] = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>(reinterpret_cast<const char*>(a.W) + ((size_t)gg[h] * KC + wk * NL) * 1024), (short)0,
+          NL * 1024, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+#pragma unroll
+      for (int h = 0; h < GPW; ++h) wf[h][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc[h], lane * 16, j * 1024, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  ZMI_WAIT_VM(GPW * NL);  // the first tile's rows and epilogue operands (issued before the weights)
+
+  // tile rt, its rows in buffer rt & 1; returns whether another tile follows (its DMA then in flight)
+  const int rt_first = rt;
+  auto run_tile = [&]() {
+    __builtin_amdgcn_s_barrier();  // tile rt's rows are in LDS for every wave; tile rt - 1's buffer is free
+    __builtin_amdgcn_sched_barrier(0);
+    const int ti = rt - rt_first;
+    if (ti == 0) ZMI_GSTAMP(1);
+    if (ti == 1) ZMI_GSTAMP(2);
+    const int row0 = rt * RT, rows = min(RT, a.M - row0);
+    const bool more = rt + 1 < rt_end;
+    if (more) {  // the next tile's epilogue operands, then its rows, under this tile's chains
+      load_epi(rt + 1, res_nxt, qp_nxt, qk_nxt);
+      dma_tile(rt + 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4_t acc0[GPW], acc1[GPW];
+#pragma unroll
+    for (int h = 0; h < GPW; ++h) acc0[h] = acc1[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    {
+      const bf16_t* xa = xs + (rt & 1) * RT * XROW + (lane & 15) * XROW + wk * NL * 64 + (lane >> 4) * 8;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const bf16x8_t x0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(xa + j * 64));
+        const bf16x8_t x1 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(xa + j * 64 + 32));
+#pragma unroll
+        for (int h = 0; h < GPW; ++h) {
+          const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[h][j]);
+          acc0[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, wv, acc0[h], 0, 0, 0);
+          acc1[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, wv, acc1[h], 0, 0, 0);
+        }
+      }
+    }
+    {
+      const int c = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+      for (int h = 0; h < GPW; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = acc0[h][q] + ror8(acc1[h][q]);
+          if (c < 8) red[(((gs + NGS * h) * W + wk) * 8 + c) * RT + rb + q] = v;
+        }
+    }
+    if (ti == 1) ZMI_GSTAMP(3);
+    __syncthreads();
+    if (ti == 1) ZMI_GSTAMP(4);
+    if (ew) {
+      auto colsum = [&](int c, int r) {  // segment sums in segment order (gemv_body's wave order)
+        float v = red[((wave * W) * 8 + c) * RT + r];
+#pragma unroll
+        for (int w = 1; w < W; ++w) v += red[((wave * W + w) * 8 + c) * RT + r];
+        return v;
+      };
+      epilogue<EPI, RT, 0>(a, colsum, lane, rows, row0, eg, res_cur, qp_cur, qk_cur, QkvFuse{nullptr, 0});
+    }
+    if (ti == 1) ZMI_GSTAMP(5);
+    return more;
+  };
+  // the first tile apart from the loop: its chains wait for each weight chunk on its own (inside the loop
+  // the compiler would wait for the whole slice before the first tile)
+  bool more = run_tile();
+  while (more) {
+    ++rt;
+    ZMI_WAIT_VM(0);  // the next tile's rows and operands (the loop-top barrier also orders the segment sums)
+    if (rt - rt_first == 2) ZMI_GSTAMP(6);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) res_cur[i] = res_nxt[i];
+    qp_cur = qp_nxt;
+    qk_cur = qk_nxt;
+    more = run_tile();
+  }
+  ZMI_GSTAMP(7);
+}
+
 
 // row tiles per workgroup: enough workgroups to fill the chip (~4 per CU), each re-reading its weight
 // slice as few times as that allows (speed only: a row's arithmetic does not depend on it)
@@ -679,11 +862,29 @@ hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
   return once ? launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 0>(a, s);
 }
 
+template <int EPI, int GPW>
+hipError_t launch_rows(const ZmiGemvArgs& a, hipStream_t s) {
+  auto fn = gemm_rows_kernel<EPI, GPW>;
+  const int n_cb = (a.N / 8 + GR_G - 1) / GR_G;
+  const int n_rt = (a.M + GR_RT - 1) / GR_RT;
+  const int rpw = rows_per_wg(n_cb, n_rt, zmi_cu_count());  // one workgroup per CU
+  const int64_t blocks = (int64_t)((n_cb + 7) / 8) * 8 * ((n_rt + rpw - 1) / rpw);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+  if (attr != hipSuccess) return attr;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(GR_G * 4 / GPW * 64), GR_LDS, s, a, n_cb, n_rt, rpw);
+  return hipGetLastError();
+}
+
 template <int EPI>
 hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
   Shape sh;
   if (!shape_for(a.K, a.ln_w != nullptr, &sh)) return hipErrorInvalidValue;
   const int g = groups_for(a, sh);
+  if (a.K == 2048 && a.M > GR_RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO && a.groups == 0 &&
+      zmi_option(ZMI_OPT_GEMM_ROWS))
+    return zmi_option(ZMI_OPT_GEMM_ROWS) == 2 ? launch_rows<EPI, 2>(a, s) : launch_rows<EPI, 4>(a, s);
   if (g == 4 && sh.W == 4 && sh.NL == 8 && sh.RT == 16 && a.M > sh.RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO)
     return launch_p<4, 4, 8, 16, PRO_PLAIN, EPI, 0>(a, s);  // groups_for's many-row plain case only
 #define ZMI_SHAPE(G_, W_, NL_, RT_) \
