@@ -330,8 +330,9 @@ int zmi_version(void);
 /* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
  *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the
  *   dispatcher spreads their workgroups evenly over the CUs instead of packing several onto one CU.
- *   ZMI_OPT_GEMM_ROWS (default 1): plain K = 2048 GEMVs over more than 16 rows run the many-row form (64 columns
- *   per workgroup, double-buffered activation tiles) instead of the 32-column tile loop. */
+ *   ZMI_OPT_GEMM_ROWS (default 1): plain K = 2048 GEMVs over many rows run the many-row form (64 columns per
+ *   workgroup, activation tiles DMA'd two ahead, one barrier per tile) where it measured faster than the
+ *   32-column tile loop; 0 = always the tile loop. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_COUNT = 2 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);

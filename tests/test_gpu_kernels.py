@@ -93,17 +93,18 @@ def test_gemv_is_batch_invariant(K, ln):
 PROD_SHAPES = {  # Zonos-v0.1 decode GEMVs: (N, K, LayerNorm'd, epilogue, pack mode)
     "qkv": (3072, 2048, True, "qkv", 0), "out_proj": (2048, 2048, False, "f32", 0),
     "fc1": (16384, 2048, True, "swiglu", 1), "fc2": (2048, 8192, False, "f32", 0),
-    "heads": (9248, 2048, True, "f32", 0)}
+    "heads": (9248, 2048, True, "f32", 0), "out_proj_residual": (2048, 2048, False, "residual", 0),
+    "fc2_residual": (2048, 8192, False, "residual", 0)}
 
 
 @pytest.mark.parametrize("name", list(PROD_SHAPES))
 def test_gemv_batch_invariant_production_shapes(name):
-    """The many-row GEMV geometries (4 column groups of 1024 threads, several row tiles per workgroup
-    with the next tile's rows DMA'd under the current one, per-shape workgroup targets) give every
-    row the bits of the decode-step launch (1-16 rows, single tile, LayerNorm prologue) at the
-    production shapes, epilogues included; the many-row plan LayerNorms its rows once per layer
-    (zmi_layernorm_rows), the decode plan in the GEMV prologue: generate_batch == generate rests
-    on exactly this."""
+    """The many-row GEMV geometries (the K = 2048 many-row form with its tiles DMA'd two ahead, or the
+    4-column-group tile loop, by row count and width; per-shape workgroup targets) give every row the bits
+    of the decode-step launch (1-16 rows, single tile, LayerNorm prologue) at the production shapes,
+    epilogues included; the many-row plan LayerNorms its rows once per layer (zmi_layernorm_rows), the
+    decode plan in the GEMV prologue: generate_batch == generate rests on exactly this. The row ranges
+    cross the many-row form's selection bounds (32, 64 rows)."""
     from zonos_vibes_amd.engine import rope_table
     L = _lib()
     N, K, ln, epi, mode = PROD_SHAPES[name]
@@ -115,6 +116,7 @@ def test_gemv_batch_invariant_production_shapes(name):
     rope = rope_table(128).to(DEV)
     smax = 160
     pos_all = torch.randint(0, smax, (big,), generator=torch.Generator().manual_seed(34), dtype=torch.int32).to(DEV)
+    res_all = rnd(big, N, scale=4.0, seed=35)
 
     def run(lo, hi, pre_ln):
         m = hi - lo
@@ -134,6 +136,10 @@ def test_gemv_batch_invariant_production_shapes(name):
             out = torch.zeros(m, N // 2, dtype=torch.bfloat16, device=DEV)
             gemv(W, xs, L.EPI_SWIGLU, out, N // 2, ln=use_ln, packed=packed)
             return (out,)
+        if epi == "residual":  # out holds the residual stream x on entry, x + bf16(linear(h)) on exit
+            out = res_all[lo:hi].clone()
+            gemv(W, xs, L.EPI_RESIDUAL, out, N, ln=use_ln, packed=packed)
+            return (out,)
         q = torch.zeros(m, 2048, dtype=torch.bfloat16, device=DEV)
         kc = torch.zeros(m, 4, smax, 128, dtype=torch.bfloat16, device=DEV)
         vt = torch.zeros(m, 4, 128, smax, dtype=torch.bfloat16, device=DEV)
@@ -147,7 +153,8 @@ def test_gemv_batch_invariant_production_shapes(name):
         return q, kc, vt
 
     ref = run(0, big, ln)
-    for lo, hi in [(0, 2), (0, 16), (6, 8), (5, 21), (100, 116), (126, 128), (16, 128), (0, 64)]:
+    for lo, hi in [(0, 2), (0, 16), (6, 8), (5, 21), (100, 116), (126, 128), (16, 128), (0, 64), (3, 36), (60, 125),
+                   (1, 66)]:
         got = run(lo, hi, ln and hi - lo > 4)
         for r, g in zip(ref, got):
             assert torch.equal(g, r[lo:hi]), (name, lo, hi)

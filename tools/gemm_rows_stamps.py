@@ -4,9 +4,9 @@
     ZMI_LIB_PATH=zonos_vibes_amd/var/libzonos_gemv_stamps.so python tools/gemm_rows_stamps.py [--slots 64]
 
 Runs the multi-slot decode plan (attention included, fused blocks off) at `--pos` and stamps the GEMVs of
-the first `--layers` layers. Stamps (s_memrealtime, 10 ns) per workgroup: 0 start, 1 first tile's rows in
-LDS, 2 second tile's rows in, 3 its chains done, 4 its segment-sum barrier passed, 5 its epilogue done,
-6 third tile's rows landed (before the barrier), 7 end. Per launch: the median of each stamp after
+the first `--layers` layers. Stamps (s_memrealtime, 10 ns) per workgroup: 0 start,
+2 second tile's start, 3 its chains done, 4 its barrier passed, 5 its epilogue done, 7 end (stamp 1: the first
+tile's chains done). Per launch: the median of each stamp after
 the first workgroup's start and the last end (us).
 """
 import argparse

@@ -604,23 +604,46 @@ __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, i
 // Many-row form of the K = 2048 GEMV (multi-slot decode and prefill, M > 16), the same per-row arithmetic as
 // gemv_body's (W, NL, RT) = (4, 8, 16) shape: a wave's chain of MFMAs over one k-segment (k-half 0 / 1 in
 // two accumulators, acc0 + ror8(acc1)), then the 4 segment sums in segment order, then epilogue().
-// What changes is the reuse: a workgroup owns 8 groups (64 columns) and each wave GPW of them over one
-// segment (GPW x 32 weight VGPRs), so every activation tile it stages serves 64 columns (gemv_body's 4-group
-// form: 32, twice the activation traffic per column) and each A fragment read from LDS feeds GPW groups; the
-// activation tiles are double-buffered, the next tile's DMA issued as the current tile's chains start.
-// Group gi's epilogue runs on wave gi (the first 8 waves: two or one per SIMD). One workgroup per CU.
+// What changes is the reuse and the pipelining:
+//  * a workgroup owns 8 groups (64 columns) and each wave GPW of them over one segment (GPW x 32 weight
+//    VGPRs), so every activation tile it stages serves 64 columns (gemv_body's 4-group form: 32, twice the
+//    activation traffic per column) and each A fragment read from LDS feeds GPW groups;
+//  * the activation tiles (and the epilogue operands) come by LDS-DMA two tiles ahead into two buffers;
+//  * one barrier per tile: group gi's epilogue runs on wave gi after it, while the other waves start the
+//    next tile's chains; an LDS arrival counter keeps those from overwriting the segment sums before every
+//    epilogue of the tile has read them.
+// One workgroup per CU.
 constexpr int GR_G = 8, GR_RT = 16, GR_XROW = 2048 + 8;
-constexpr size_t GR_RED = (size_t)2 * GR_RT * GR_XROW * 2;
-constexpr size_t GR_LDS = GR_RED + (size_t)GR_G * 4 * 8 * GR_RT * 4;
+constexpr size_t GR_RED = (size_t)2 * GR_RT * GR_XROW * 2;             // after the two activation tiles
+constexpr size_t GR_OPS = GR_RED + (size_t)GR_G * 4 * 8 * GR_RT * 4;   // epilogue operands, 2 x 2 KiB
+constexpr size_t GR_CNT = GR_OPS + 2 * 2048;
+constexpr size_t GR_LDS = GR_CNT + 16;
+
+// one 256-byte LDS-DMA piece (64 lanes x 4 B, lane-linear)
+__device__ __forceinline__ void dma_dword(const void* gsrc, void* ldp) {
+  const unsigned ldst =
+      __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) void*)ldp);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(ldst)
+               : "memory");
+}
 
 template <int EPI, int GPW>
 __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const ZmiGemvArgs a, int n_cb, int n_rt,
                                                                         int rpw) {
   constexpr int W = 4, NL = 8, RT = GR_RT, K = 2048, KC = K / 64, XROW = GR_XROW, NE = 2;
   constexpr int NGS = GR_G / GPW, NWV = NGS * W, PPW = RT * (K / 512) / NWV;  // group sets, waves, DMA pieces / wave
+  // operand pieces per tile, issued by the last wave: residual inputs (16 rows x 8 groups x 16 B), or the rows'
+  // positions and cache rows (dwords)
+  constexpr int EP = EPI == ZMI_EPI_RESIDUAL ? 2 : (EPI == ZMI_EPI_QKV ? 1 : 0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);                 // [2][RT][XROW] activation tiles
   float* red = reinterpret_cast<float*>(smem + GR_RED);          // [group][segment][8][RT] segment sums
+  char* ops = smem + GR_OPS;                                     // [2][2 KiB]
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + GR_CNT);    // epilogues finished
   const int b = blockIdx.x, idx = b >> 3;
   const int n_rg = (n_rt + rpw - 1) / rpw;
   const int cb = (idx / n_rg) * 8 + (b & 7), rg = idx - (idx / n_rg) * n_rg;  // gemv_body's XCD-aware map
@@ -633,15 +656,17 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
   int gg[GPW];
 #pragma unroll
   for (int h = 0; h < GPW; ++h) gg[h] = min(cb * GR_G + gs + NGS * h, ngroups - 1);  // clamped: discarded
-  // the epilogue of group eg = wave (waves 0..7)
-  const bool ew = wave < GR_G && cb * GR_G + wave < ngroups;
+  const int n_ew = min(GR_G, ngroups - cb * GR_G);  // epilogue waves: group cb * 8 + wave on wave < n_ew
+  const bool ew = wave < n_ew;
   const int eg = cb * GR_G + wave;
-  int rt = rg * rpw;
-  const int rt_end = min(n_rt, rt + rpw);
+  const int t0 = rg * rpw;
+  const int rt_end = min(n_rt, t0 + rpw);
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X);
+  const bool opw = EP && wave == NWV - 1;  // the operand-piece wave
+  if (tid == 0) *cnt = 0;
 
-  // a tile = 16 rows x 4 KiB = 64 DMA pieces, PPW per wave (rows past M re-read row M - 1: their outputs are
-  // discarded, and every wave issues the same count, which the vmcnt waits below rely on)
+  // tile t = 16 rows x 4 KiB = 64 DMA pieces, PPW per wave (rows past M re-read row M - 1: their outputs are
+  // discarded, and the waves' counts are fixed, which the vmcnt waits rely on), then its epilogue operands
   auto dma_tile = [&](int t) {
     bf16_t* dst = xs + (t & 1) * RT * XROW;
 #pragma unroll
@@ -650,32 +675,24 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
       const int sr = min(t * RT + r, a.M - 1);
       dma_piece(X + (size_t)sr * a.ldx + p * 512 + lane * 8, dst + r * XROW + p * 512);
     }
-  };
-  // epilogue operands of tile t (epilogue waves): the group's residual inputs, the row's position / cache row
-  auto load_epi = [&](int t, uint32_t(&res)[NE], int& qp, int& qk) {
-    const int row0 = t * RT, rows = min(RT, a.M - row0);
+    if (opw) {
+      char* od = ops + (t & 1) * 2048;
+      if (EPI == ZMI_EPI_RESIDUAL) {  // [row][group] 16 B: out[row][8 g .. 8 g + 7]
 #pragma unroll
-    for (int i = 0; i < NE; ++i) res[i] = 0;
-    qp = -1;
-    qk = 0;
-    if (!ew) return;
-    if (EPI == ZMI_EPI_RESIDUAL) {
-#pragma unroll
-      for (int i = 0; i < NE; ++i) {
-        const int e = lane + 64 * i, r = e >> 3, n = eg * 8 + (e & 7);
-        if (r < rows && n < a.n_valid) res[i] = reinterpret_cast<const bf16_t*>(a.out)[(size_t)(row0 + r) * a.ldo + n];
+        for (int i = 0; i < 2; ++i) {
+          const int e = lane + 64 * i, r = e >> 3, gi = min(cb * GR_G + (e & 7), ngroups - 1);
+          dma_piece(reinterpret_cast<const bf16_t*>(a.out) + (size_t)min(t * RT + r, a.M - 1) * a.ldo + gi * 8,
+                    reinterpret_cast<bf16_t*>(od + i * 1024));
+        }
+      } else if (EPI == ZMI_EPI_QKV) {  // dwords 0..15 the rows' positions, 16..31 their cache rows
+        const int r = min(t * RT + (lane & 15), a.M - 1);
+        dma_dword((lane & 16) ? a.row_kv + r : a.row_pos + r, od);
       }
-    }
-    if (EPI == ZMI_EPI_QKV && (lane >> 2) < rows) {
-      qp = a.row_pos[row0 + (lane >> 2)];
-      qk = a.row_kv[row0 + (lane >> 2)];
     }
   };
 
-  uint32_t res_cur[NE], res_nxt[NE];
-  int qp_cur, qk_cur, qp_nxt = -1, qk_nxt = 0;
-  dma_tile(rt);
-  load_epi(rt, res_cur, qp_cur, qk_cur);
+  dma_tile(t0);
+  if (t0 + 1 < rt_end) dma_tile(t0 + 1);
   __builtin_amdgcn_sched_barrier(0);
   // the weight slices of the wave's groups (GPW NL x 16 B per lane), in flight at once, in chain order (chunk
   // j of every group before chunk j + 1): the first tile's chains follow them as they land. Re-read by the
@@ -694,28 +711,25 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
       for (int h = 0; h < GPW; ++h) wf[h][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc[h], lane * 16, j * 1024, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
-  ZMI_WAIT_VM(GPW * NL);  // the first tile's rows and epilogue operands (issued before the weights)
+  // the first tile's pieces: issued before the second tile's and the weights
+  if (t0 + 1 >= rt_end)
+    ZMI_WAIT_VM(GPW * NL);
+  else if (opw)
+    ZMI_WAIT_VM(GPW * NL + PPW + EP);
+  else
+    ZMI_WAIT_VM(GPW * NL + PPW);
+  __syncthreads();
 
-  // tile rt, its rows in buffer rt & 1; returns whether another tile follows (its DMA then in flight)
-  const int rt_first = rt;
-  auto run_tile = [&]() {
-    __builtin_amdgcn_s_barrier();  // tile rt's rows are in LDS for every wave; tile rt - 1's buffer is free
-    __builtin_amdgcn_sched_barrier(0);
-    const int ti = rt - rt_first;
-    if (ti == 0) ZMI_GSTAMP(1);
+  for (int t = t0;; ++t) {  // invariant: tile t's rows and operands are in LDS, visible to every wave
+    const int ti = t - t0;
     if (ti == 1) ZMI_GSTAMP(2);
-    const int row0 = rt * RT, rows = min(RT, a.M - row0);
-    const bool more = rt + 1 < rt_end;
-    if (more) {  // the next tile's epilogue operands, then its rows, under this tile's chains
-      load_epi(rt + 1, res_nxt, qp_nxt, qk_nxt);
-      dma_tile(rt + 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    const int row0 = t * RT, rows = min(RT, a.M - row0);
+    const bool more = t + 1 < rt_end;
     f32x4_t acc0[GPW], acc1[GPW];
 #pragma unroll
     for (int h = 0; h < GPW; ++h) acc0[h] = acc1[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     {
-      const bf16_t* xa = xs + (rt & 1) * RT * XROW + (lane & 15) * XROW + wk * NL * 64 + (lane >> 4) * 8;
+      const bf16_t* xa = xs + (t & 1) * RT * XROW + (lane & 15) * XROW + wk * NL * 64 + (lane >> 4) * 8;
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
         const bf16x8_t x0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(xa + j * 64));
@@ -728,6 +742,14 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
         }
       }
     }
+    if (ti == 0) ZMI_GSTAMP(1);
+    if (ti == 1) ZMI_GSTAMP(3);
+    // the previous tile's epilogues have read the segment sums (bounded: they are a few hundred cycles of work)
+    if (ti > 0) {
+      const unsigned want = (unsigned)(n_ew * ti);
+      for (int spin = 0; *reinterpret_cast<volatile unsigned*>(cnt) < want && spin < (1 << 20); ++spin)
+        __builtin_amdgcn_s_sleep(1);
+    }
     {
       const int c = lane & 15, rb = (lane >> 4) * 4;
 #pragma unroll
@@ -738,9 +760,27 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
           if (c < 8) red[(((gs + NGS * h) * W + wk) * 8 + c) * RT + rb + q] = v;
         }
     }
-    if (ti == 1) ZMI_GSTAMP(3);
-    __syncthreads();
+    // this tile's epilogue operands into registers before the buffer is re-filled
+    uint32_t res_pre[NE] = {0u, 0u};
+    int q_pos = -1, q_kvr = 0;
+    if (ew) {
+      const char* od = ops + (t & 1) * 2048;
+      if (EPI == ZMI_EPI_RESIDUAL) {
+#pragma unroll
+        for (int i = 0; i < NE; ++i) {
+          const int e = lane + 64 * i, r = e >> 3, c = e & 7;
+          res_pre[i] = *reinterpret_cast<const uint16_t*>(od + (r * GR_G + wave) * 16 + c * 2);
+        }
+      }
+      if (EPI == ZMI_EPI_QKV && (lane >> 2) < rows) {
+        q_pos = reinterpret_cast<const int*>(od)[lane >> 2];
+        q_kvr = reinterpret_cast<const int*>(od)[16 + (lane >> 2)];
+      }
+    }
+    ZMI_WAIT_VM(0);  // the next tile's pieces
+    __syncthreads();  // segment sums complete; the next tile's rows visible; this tile's buffers free
     if (ti == 1) ZMI_GSTAMP(4);
+    if (t + 2 < rt_end) dma_tile(t + 2);
     if (ew) {
       auto colsum = [&](int c, int r) {  // segment sums in segment order (gemv_body's wave order)
         float v = red[((wave * W) * 8 + c) * RT + r];
@@ -748,23 +788,11 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
         for (int w = 1; w < W; ++w) v += red[((wave * W + w) * 8 + c) * RT + r];
         return v;
       };
-      epilogue<EPI, RT, 0>(a, colsum, lane, rows, row0, eg, res_cur, qp_cur, qk_cur, QkvFuse{nullptr, 0});
+      epilogue<EPI, RT, 0>(a, colsum, lane, rows, row0, eg, res_pre, q_pos, q_kvr, QkvFuse{nullptr, 0});
+      if (more && lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (ti == 1) ZMI_GSTAMP(5);
-    return more;
-  };
-  // the first tile apart from the loop: its chains wait for each weight chunk on its own (inside the loop
-  // the compiler would wait for the whole slice before the first tile)
-  bool more = run_tile();
-  while (more) {
-    ++rt;
-    ZMI_WAIT_VM(0);  // the next tile's rows and operands (the loop-top barrier also orders the segment sums)
-    if (rt - rt_first == 2) ZMI_GSTAMP(6);
-#pragma unroll
-    for (int i = 0; i < NE; ++i) res_cur[i] = res_nxt[i];
-    qp_cur = qp_nxt;
-    qk_cur = qk_nxt;
-    more = run_tile();
+    if (!more) break;
   }
   ZMI_GSTAMP(7);
 }
@@ -862,6 +890,12 @@ hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
   return once ? launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_PLAIN, EPI, 0>(a, s);
 }
 
+// where the many-row form beats gemv_body's 4-group tile loop (C3 decode shapes, tools/kernel_bench.py
+// --gemm-rows 1,0): 128 rows qkv 18.1 -> 13.0 us, fc1 41.9 -> 31.1, heads 36.9 -> 24.0, out_proj 9.8 -> 7.0;
+// 64 rows qkv 12.1 -> 9.6, fc1 26.2 -> 22.8, heads 21.3 -> 15.3 but out_proj 5.8 -> 6.8; 32 rows only the
+// wide ones (heads 13.3 -> 11.6; qkv 7.6 -> 9.7, out_proj 5.8 -> 8.3)
+inline bool rows_form(int M, int N) { return M > 64 || (M > 32 && N >= 3072) || N >= 8192; }
+
 template <int EPI, int GPW>
 hipError_t launch_rows(const ZmiGemvArgs& a, hipStream_t s) {
   auto fn = gemm_rows_kernel<EPI, GPW>;
@@ -883,8 +917,8 @@ hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
   if (!shape_for(a.K, a.ln_w != nullptr, &sh)) return hipErrorInvalidValue;
   const int g = groups_for(a, sh);
   if (a.K == 2048 && a.M > GR_RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO && a.groups == 0 &&
-      zmi_option(ZMI_OPT_GEMM_ROWS))
-    return zmi_option(ZMI_OPT_GEMM_ROWS) == 2 ? launch_rows<EPI, 2>(a, s) : launch_rows<EPI, 4>(a, s);
+      zmi_option(ZMI_OPT_GEMM_ROWS) && rows_form(a.M, a.N))
+    return launch_rows<EPI, 2>(a, s);
   if (g == 4 && sh.W == 4 && sh.NL == 8 && sh.RT == 16 && a.M > sh.RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO)
     return launch_p<4, 4, 8, 16, PRO_PLAIN, EPI, 0>(a, s);  // groups_for's many-row plain case only
 #define ZMI_SHAPE(G_, W_, NL_, RT_) \
