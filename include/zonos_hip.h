@@ -144,6 +144,20 @@ int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* a
  * *err becomes nonzero if a wait gave up. */
 int zmi_ffn_block(const ZmiGemvArgs* out_proj, const ZmiGemvArgs* fc1, void* gran, unsigned* err, void* stream);
 int64_t zmi_ffn_block_gran_words(int rows);
+/* Fused decode launch of a block after its QKV projection (reference _torch.py:136 attention, :140 out_proj,
+ * :100-101 residual + norm2, :147-152 fc1 + SwiGLU) for 1 <= M rows with M x hkv <= 8 and positions
+ * <= zmi_attn_ffn_max_pos(): the chunk-split attention of zmi_attn_block over the KV cache (q, K / V as the
+ * preceding zmi_gemv_launch(qkv, EPI_QKV) left them: `qkv` is that launch's argument block), then out_proj
+ * (EPI_RESIDUAL, X = attn_out) and the LayerNorm'd fc1 (EPI_SWIGLU), in ONE launch of 256 workgroups (one
+ * per CU; needs 256 CUs) whose weight streams run under the attention chain. attn_out (bf16 [M][ldo]), x and
+ * h are bit-identical to zmi_attn_block(SPLIT) + zmi_ffn_block, i.e. to zmi_attention + two zmi_gemv_launch.
+ * Granule areas of {value, tag = position + 1} words (zero a row's words when it starts a new utterance):
+ * xgran zmi_attn_block_gran_words(M, hkv), ogran and rgran zmi_attn_ffn_gran_words(M) each (rgran may be
+ * zmi_ffn_block's area). out_proj->row_pos = qkv->row_pos. *err becomes nonzero if a wait gave up. */
+int zmi_attn_ffn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* out_proj, const ZmiGemvArgs* fc1, void* xgran,
+                       void* ogran, void* rgran, unsigned* err, void* attn_out, int ldo, void* stream);
+int64_t zmi_attn_ffn_gran_words(int rows);
+int zmi_attn_ffn_max_pos(void);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);
@@ -332,8 +346,11 @@ int zmi_version(void);
  *   dispatcher spreads their workgroups evenly over the CUs instead of packing several onto one CU.
  *   ZMI_OPT_GEMM_ROWS (default 1): plain K = 2048 GEMVs over many rows run the many-row form (64 columns per
  *   workgroup, activation tiles DMA'd two ahead, one barrier per tile) where it measured faster than the
- *   32-column tile loop; 0 = always the tile loop. */
-enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_COUNT = 2 };
+ *   32-column tile loop; 0 = always the tile loop.
+ *   ZMI_OPT_AF_DEPTH (default 3): weight loads each streaming wave of zmi_attn_ffn_block keeps in flight (1 KiB
+ *          each; 2, 3, 4, 6 or 0 = unthrottled): the launch's latency-bound hand-offs queue behind whatever the
+ *          chip has in flight, so the weight stream is issued progressively. */
+enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_COUNT = 4 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

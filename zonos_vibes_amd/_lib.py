@@ -19,6 +19,8 @@ c_int_p = ctypes.POINTER(ctypes.c_int)
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
 OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
 OPT_GEMM_ROWS = 1
+OPT_AF_DEPTH = 2
+OPT_AF_DELAY = 3
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
@@ -99,6 +101,10 @@ _SIGS = {
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
     "zmi_ffn_block_gran_words": (c_int64, [c_int]),
+    "zmi_attn_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs),
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "zmi_attn_ffn_gran_words": (c_int64, [c_int]),
+    "zmi_attn_ffn_max_pos": (c_int, []),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,
                                   ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),

@@ -114,6 +114,12 @@ class HipEngine:
         # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= 16 rows at the v0.1 dims on a 256-CU device:
         # fc1's weights stream while the out_proj chain runs (identical bits)
         self.ffn_block = True
+        # attention + out_proj + fc1 as ONE launch after a plain QKV launch (zmi_attn_ffn_block) for <= 2 rows
+        # (batch 1) at positions < 1024: out_proj's and fc1's weights stream under the attention chain
+        # (identical bits). Off: measured slower (C2 step 1042-1075 us against 984, tools/step_ab.py; every
+        # hand-off of the chain takes 3-5 us under the weight stream against ~1.5 on an idle memory system,
+        # DESIGN.md §5)
+        self.attn_ffn = False
         self._plans: dict[tuple, list] = {}
         self._graphs: dict[tuple, int] = {}
         # host-side upper bound of each slot's next decode position (prefill sets it, every step adds 1):
@@ -154,6 +160,8 @@ class HipEngine:
             self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block
             # zmi_ffn_block hand-off granules (the new residual rows), one area per layer
             self.ffn_gran = z(self.L, R, self.lib.zmi_ffn_block_gran_words(1), dt=torch.int64)
+            # zmi_attn_ffn_block hand-off granules (the attention output rows), one area per layer
+            self.attn_gran = z(self.L, R, self.lib.zmi_attn_ffn_gran_words(1), dt=torch.int64)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -267,6 +275,10 @@ class HipEngine:
         return (self.ffn_block and rows <= 16 and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
                 and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
 
+    def _use_attn_ffn(self, rows: int, form: str) -> bool:
+        return (self.attn_ffn and form == "split" and rows * self.Hkv <= 8 and rows <= 4 and self._use_ffn_block(rows)
+                and self.H == 4 * self.Hkv and self.hd == 128)
+
     def _forms(self, rows: int) -> list:
         """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
         QKV and attention launches (any position)."""
@@ -323,6 +335,20 @@ class HipEngine:
 
             for i, lw in enumerate(w["layers"]):
                 kv = (self.kc[i], self.vc[i])
+                if self._use_attn_ffn(rows, form):
+                    # QKV launch, then attention + out_proj + fc1 in one launch, then fc2
+                    qkv = self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                     ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
+                    plan.append(("gemv", qkv))
+                    o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
+                    o_item[0].row_pos = self.row_pos.data_ptr()
+                    f_item = self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
+                                        ln=(lw["ln2_w"], lw["ln2_b"]))
+                    qa = _lib.GemvArgs.from_buffer_copy(qkv[0])
+                    qa.row_kv = None  # decode: query row r caches into KV row r (one dependent load fewer)
+                    plan.append(("attnffn", (qa, o_item[0], f_item[0], i)))
+                    plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
+                    continue
                 xin, ln = normed((lw["ln1_w"], lw["ln1_b"])) if not fused else (self.x, (lw["ln1_w"], lw["ln1_b"]))
                 qkv = self._gemv(lw["qkv"], xin, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                  ln=ln, kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
@@ -370,6 +396,13 @@ class HipEngine:
                                               self.attn.data_ptr(), self.H * self.hd, slices,
                                               ctypes.byref(pf), self.sptr), "attn_block")
 
+    def _run_attn_ffn(self, item):
+        a, o, f, i = item
+        _lib.check(self.lib.zmi_attn_ffn_block(ctypes.byref(a), ctypes.byref(o), ctypes.byref(f),
+                                               self.blk_gran[i].data_ptr(), self.attn_gran[i].data_ptr(),
+                                               self.ffn_gran[i].data_ptr(), self.blk_err[4:].data_ptr(),
+                                               self.attn.data_ptr(), self.H * self.hd, self.sptr), "attn_ffn_block")
+
     def _run_ffn_block(self, item):
         o, f, i = item
         _lib.check(self.lib.zmi_ffn_block(ctypes.byref(o), ctypes.byref(f), self.ffn_gran[i].data_ptr(),
@@ -379,11 +412,11 @@ class HipEngine:
         """Raise if a launch gave up waiting on an in-launch hand-off (bounded spin) or refused a row past
         its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
         attn = int(self.attn_work[:4].view(torch.int32).item())
-        blk, mamba, _, ffn = (int(v) for v in self.blk_err[:4].tolist())
-        if attn or blk or mamba or ffn:
+        blk, mamba, _, ffn, af = (int(v) for v in self.blk_err[:5].tolist())
+        if attn or blk or mamba or ffn or af:
             self.attn_work[:4].zero_()
             self.blk_err[:2].zero_()
-            self.blk_err[3:4].zero_()
+            self.blk_err[3:5].zero_()
             self.stream.synchronize()
         if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
@@ -394,6 +427,9 @@ class HipEngine:
             raise RuntimeError("mamba_block: a wait for the in_proj output timed out (results are invalid)")
         if ffn:
             raise RuntimeError("ffn_block: a wait for the new residual rows timed out (results are invalid)")
+        if af:
+            raise RuntimeError("attn_ffn_block: a hand-off wait timed out or a row was past the form's reach "
+                               "(results are invalid)")
 
     def refresh_inputs(self):
         """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
@@ -431,6 +467,8 @@ class HipEngine:
                 self._run_attn_block(item)
             elif kind == "ffnblk":
                 self._run_ffn_block(item)
+            elif kind == "attnffn":
+                self._run_attn_ffn(item)
             elif kind == "attn":
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
                 self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
@@ -520,6 +558,7 @@ class HipEngine:
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
         self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
         self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
+        self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
 
     def _prefill_logits(self, s_len: int):
         """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""
