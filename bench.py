@@ -305,6 +305,38 @@ def hybrid_step_bytes(e, pos: int) -> int:
     return w + state + kv
 
 
+def time_default_capacity(dev, n_new: int, ref_codes) -> dict:
+    """The C2 utterance through a model whose engine is sized for the reference's default
+    generate(max_new_tokens=86 * 30) (reference zonos/model.py:223): the decode forms are picked per step from
+    the rows' positions, not from the capacity, so the step and the codes must match the C2 line's."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    cap = 86 * 30
+    m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + cap + 9, max_prefill=LC + 1)
+    cond = cond_tensor(1, cfg.backbone.d_model, dev)
+
+    def one():
+        codes = m.generate(cond, max_new_tokens=n_new, sampling_params=dict(temperature=0.0), progress_bar=False,
+                           chunk=128)
+        return codes, m.autoencoder.decode(codes)
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes, _ = one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    us, pos = time_decode_step(m, cond)
+    out = {"config": f"C2 utterance ({n_new} frames, greedy, EOS suppressed) through an engine sized for the reference "
+                     f"default max_new_tokens={cap} (KV capacity {m.engine.smax} positions)",
+           "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3), "utterance_ms": round(el * 1e3, 1),
+           "decode_step_us": round(us, 1), "decode_step_pos": pos,
+           "codes_equal_c2": bool(torch.equal(codes, ref_codes))}
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
 def time_hybrid(dev, n_new: int) -> dict:
     """BASELINE config C4 (Zonos-v0.1-hybrid, batch 1, one GPU): one C2-shaped utterance (Lc 160, n_new
     frames, greedy, EOS suppressed) through generate() + DAC decode, wall-clock RTF, and the decode step
@@ -457,7 +489,7 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
     return res
 
 
-def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430) -> dict:
+def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430, engine_opts: dict | None = None) -> dict:
     """One GPU's share of BASELINE config C5 (voice clone, long form): `slots` utterances of n_new frames
     (60 s) after a `prefix`-frame audio prompt (random codes), Lc = 160, greedy, EOS suppressed, through
     `slots` slots (contexts grow to Lc + prefix + n_new ~ 5.8k positions), then DAC decode of every
@@ -466,6 +498,9 @@ def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430) -> dict:
     cfg = zonos_v01_transformer()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_slots=slots, max_seqlen=LC + prefix + n_new + 9,
                         max_prefill=LC + prefix + 1)
+    for k, v in (engine_opts or {}).items():  # A/B knobs (tools/bench_c5.py)
+        setattr(m.engine, k, v)
+    m.engine._build_plan()
     g = torch.Generator().manual_seed(11)
     conds = [cond_tensor(200 + i, cfg.backbone.d_model, dev) for i in range(slots)]
     prefixes = [torch.randint(0, 1024, (1, 9, prefix), generator=g).to(dev) for _ in range(slots)]
@@ -579,6 +614,8 @@ def main():
     ap.add_argument("--no-hybrid", action="store_true", help="skip the C4 hybrid-backbone line in `widened`")
     ap.add_argument("--no-batch", action="store_true", help="skip the C3-sample batch line in `widened`")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (voice clone, 60 s, 8 slots) line in `widened`")
+    ap.add_argument("--no-default-cap", action="store_true",
+                    help="skip the line with the engine sized for the reference default max_new_tokens")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -659,6 +696,8 @@ def main():
     step_us, step_pos = time_decode_step(model, cond)
     ktab = kernel_table(model, cond)
     widened = time_widened_rows(model, dev)
+    if rank == 0 and not args.no_default_cap:
+        widened["default_capacity"] = time_default_capacity(dev, n_new, ref_codes)
     if rank == 0 and not args.no_hybrid:
         widened["hybrid_c4"] = time_hybrid(dev, n_new)
     if rank == 0 and not args.no_c5:

@@ -194,6 +194,10 @@ typedef struct ZmiSlots {
 int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, const float* noise, int* next_tokens,
                     unsigned* counters, int mode, int slot_begin, int slot_count, const void* emb, int d, void* x,
                     int* row_kv, int* row_pos, void* stream);
+/* zmi_sample_step mode 0 for a launch whose slots all sample greedily (temperature <= 0; the caller
+ * guarantees it): one workgroup per slot, no in-launch hand-off between codebooks; identical results. */
+int zmi_sample_step_greedy(const ZmiSlots* slots, const float* logits_rows, int* next_tokens, int slot_begin,
+                           int slot_count, const void* emb, int d, void* x, int* row_kv, int* row_pos, void* stream);
 /* sample_from_logits (sampling.py:117-182) on its own: logits f32 [batch][9][1026] as given (no CFG,
  * no EOS bias), optional generated_tokens int32 [batch][9][gen_len] for the repetition penalty,
  * one parameter block (device), optional exponential noise [batch][9][1026]; tokens int32 [batch][9]. */

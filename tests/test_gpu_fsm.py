@@ -16,8 +16,11 @@ DEV = "cuda"
 CASES = ["greedy_maxlen", "greedy_prefix", "greedy_eos_0", "greedy_eos_1"]
 
 
+@pytest.mark.parametrize("greedy_kernel", [False, True])
 @pytest.mark.parametrize("tag", CASES)
-def test_fsm_and_frame_write_match_reference(tag):
+def test_fsm_and_frame_write_match_reference(tag, greedy_kernel):
+    """greedy_kernel: decode steps through zmi_sample_step_greedy (one workgroup per slot) instead of
+    zmi_sample_step's per-codebook workgroups."""
     from oracle.zonos_cpu import OracleZonos
     from zonos_vibes_amd import _lib as L
     from zonos_vibes_amd.engine import SamplingParams
@@ -57,8 +60,12 @@ def test_fsm_and_frame_write_match_reference(tag):
     for i, lg in enumerate(raw):
         assert int(st["active"][0]) == 1, f"stopped after {i} of {len(raw)} sampling calls"
         rows[0] = lg[0].to(DEV)
-        L.check(lib.zmi_sample_step(ctypes.byref(sl), rows.data_ptr(), None, nxt.data_ptr(), cnt.data_ptr(),
-                                    1 if i == 0 else 0, 0, 1, None, 0, None, None, None, sp))
+        if greedy_kernel and i > 0:
+            L.check(lib.zmi_sample_step_greedy(ctypes.byref(sl), rows.data_ptr(), nxt.data_ptr(), 0, 1, None, 0,
+                                               None, None, None, sp))
+        else:
+            L.check(lib.zmi_sample_step(ctypes.byref(sl), rows.data_ptr(), None, nxt.data_ptr(), cnt.data_ptr(),
+                                        1 if i == 0 else 0, 0, 1, None, 0, None, None, None, sp))
         torch.cuda.synchronize()
     assert int(st["active"][0]) == 0, "the reference loop ended here"
     assert torch.equal(delayed[0, :, :total].cpu().long(), ref_delayed[:, :total]), tag

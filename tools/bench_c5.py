@@ -1,6 +1,6 @@
 """The bench's C5 share (8 voice-clone utterances of 60 s after a 430-frame prefix) on its own.
 
-    python tools/bench_c5.py [n_new]
+    python tools/bench_c5.py [n_new] [JSON engine options, e.g. '{"ffn_block": false}'] [slots]
 """
 import json
 import os
@@ -14,7 +14,11 @@ import bench  # noqa: E402
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 5168
-    print(json.dumps(bench.time_c5(torch.device("cuda", 0), n_new=n)), flush=True)
+    opts = json.loads(sys.argv[2]) if len(sys.argv) > 2 else {}
+    slots = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    r = bench.time_c5(torch.device("cuda", 0), slots=slots, n_new=n, engine_opts=opts)
+    r["engine_opts"] = opts
+    print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

@@ -112,6 +112,8 @@ _SIGS = {
     "zmi_attention_chunk": (c_int, []),
     "zmi_sample_step": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "zmi_sample_step_greedy": (c_int, [ctypes.POINTER(Slots), c_void_p, c_void_p, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_sample_logits": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "zmi_apply_delay_pattern": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p]),
     "zmi_revert_delay_pattern": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),

@@ -111,15 +111,23 @@ class HipEngine:
         self.prefetch_blocks = 192
         self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
-        # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= 16 rows at the v0.1 dims on a 256-CU device:
-        # fc1's weights stream while the out_proj chain runs (identical bits)
+        # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
+        # device: fc1's weights stream while the out_proj chain runs (identical bits). Above 2 rows the launch
+        # loses to the separate ones (every workgroup DMAs all rows and gathers all rows' residual granules):
+        # C5-shaped steps at 4 / 8 / 16 rows 1.21 / 1.52 / 2.06 ms without it against 1.26 / 1.61 / 2.27 with it
+        # (tools/bench_c5.py, profiles/r03_ffnblk_rows_ab.jsonl)
         self.ffn_block = True
+        self.ffn_block_rows = 2
         # attention + out_proj + fc1 as ONE launch after a plain QKV launch (zmi_attn_ffn_block) for <= 2 rows
         # (batch 1) at positions < 1024: out_proj's and fc1's weights stream under the attention chain
         # (identical bits). Off: measured slower (C2 step 1042-1075 us against 984, tools/step_ab.py; every
         # hand-off of the chain takes 3-5 us under the weight stream against ~1.5 on an idle memory system,
         # DESIGN.md §5)
         self.attn_ffn = False
+        # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
+        # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
+        self.greedy_sampler = True
+        self.slot_greedy = [False] * self.S
         self._plans: dict[tuple, list] = {}
         self._graphs: dict[tuple, int] = {}
         # host-side upper bound of each slot's next decode position (prefill sets it, every step adds 1):
@@ -272,7 +280,7 @@ class HipEngine:
         return self.attn_self_slices | _lib.ATTNBLK_SELF if form == "self" else self.attn_block_slices
 
     def _use_ffn_block(self, rows: int) -> bool:
-        return (self.ffn_block and rows <= 16 and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
+        return (self.ffn_block and rows <= self.ffn_block_rows and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
                 and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
 
     def _use_attn_ffn(self, rows: int, form: str) -> bool:
@@ -438,7 +446,17 @@ class HipEngine:
                                            self.x.data_ptr(), self.row_kv.data_ptr(), self.row_pos.data_ptr(),
                                            self.sptr), "embed")
 
+    def _greedy_step(self, slot_begin: int, count: int) -> bool:
+        return self.greedy_sampler and all(self.slot_greedy[slot_begin: slot_begin + count])
+
     def _sample(self, logits, noise, mode, slot_begin, count):
+        if mode == 0 and noise is None and self._greedy_step(slot_begin, count):
+            _lib.check(self.lib.zmi_sample_step_greedy(ctypes.byref(self.slots), logits.data_ptr(),
+                                                       self.next_tok.data_ptr(), slot_begin, count,
+                                                       self.w["emb"].data_ptr(), self.d, self.x.data_ptr(),
+                                                       self.row_kv.data_ptr(), self.row_pos.data_ptr(), self.sptr),
+                       "sample_greedy")
+            return
         _lib.check(self.lib.zmi_sample_step(ctypes.byref(self.slots), logits.data_ptr(),
                                             None if noise is None else noise.data_ptr(), self.next_tok.data_ptr(),
                                             self.samp_cnt.data_ptr(), mode, slot_begin, count,
@@ -478,15 +496,16 @@ class HipEngine:
 
     def capture(self, slots: int | None = None, form: str = "none"):
         rows = self._rows(slots)
-        if (rows, form) not in self._graphs:
+        key = (rows, form, self._greedy_step(0, rows // 2))
+        if key not in self._graphs:
             _lib.check(self.lib.zmi_graph_begin(self.sptr), "graph_begin")
             try:
                 self.enqueue_step(slots=rows // 2, form=form)
             finally:
                 g = ctypes.c_void_p()
                 _lib.check(self.lib.zmi_graph_end(self.sptr, ctypes.byref(g)), "graph_end")
-            self._graphs[(rows, form)] = g.value
-        return self._graphs[(rows, form)]
+            self._graphs[key] = g.value
+        return self._graphs[key]
 
     def _advance(self, n: int, slots: int):
         for s in range(slots):
@@ -531,6 +550,7 @@ class HipEngine:
             cp = torch.tensor(bytearray(params.to_c()), dtype=torch.uint8)
             sz = ctypes.sizeof(_lib.Sampling)
             self.params[slot * sz:(slot + 1) * sz].copy_(cp)
+            self.slot_greedy[slot] = params.temperature <= 0
             _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
             self._reset_granules(slot)  # no granule of an earlier utterance may match a tag
             xp = self.x_pre[: 2 * s_len]
