@@ -41,26 +41,31 @@ def cond_tensor(seed: int, d: int, dev, lc: int = LC):
 
 
 def time_dominant_kernel(model, reps: int = 3):
-    """The largest kernel of the C2 step, zmi_ffn_block (out_proj + residual, LayerNorm, fc1, SwiGLU: 75.5 MB
-    of weights per launch), for every layer, timed with HIP events on the engine stream one launch at a
-    time with its hand-off granules zeroed first (a re-run at the same position would find its own
-    granules). Rotating over all 26 layers' weights (2 GB) keeps the stream out of the 256 MiB Infinity
-    Cache, so the bytes come from HBM as in the decode step. Returns (us per launch, algorithmic bytes)."""
+    """The largest kernel of the C2 step, the fc1 GEMV (LayerNorm prologue + packed SwiGLU epilogue: 67.1 MB of
+    weights per launch), for every layer, timed with HIP events on the engine stream: the 26 layers' launches
+    back to back, `reps` times. Rotating over all 26 layers' weights (1.7 GB) keeps the stream out of the
+    256 MiB Infinity Cache, so the bytes come from HBM as in the decode step. Returns (us per launch,
+    algorithmic bytes)."""
     e = model.engine
-    items = [item for kind, item in e._plan(2) if kind == "ffnblk"]
-    assert items, "the C2 plan has no fused out_proj + fc1 launch"
+    items = [item for kind, item in e._plan(2) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
+    assert items, "the C2 plan has no fc1 GEMV launch"
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tot = 0.0
     with torch.cuda.stream(e.stream):
-        e.row_pos[:2] = 591
-    us = _time_fused(e, items, e.ffn_gran, e._run_ffn_block, reps)
-    with torch.cuda.stream(e.stream):
-        e.row_pos[:2] = -1
-    e.check_errors()
+        for r in range(reps + 1):
+            st.record(e.stream)
+            for it in items:
+                e._run_gemv(it)
+            en.record(e.stream)
+            en.synchronize()
+            if r:
+                tot += st.elapsed_time(en) * 1000.0
     d, F = e.d, e.F
-    bytes_launch = (d * d + 2 * F * d) * 2 + 2 * d * 2 * 3 + 2 * d * 2 + 2 * F * 2  # weights, attn/x in, x out, ln, h out
-    return us, bytes_launch
+    bytes_launch = 2 * F * d * 2 + 2 * d * 2 + 2 * d * 2 + 2 * F * 2  # weights, x rows in, ln gamma / beta, h out
+    return tot / (reps * len(items)), bytes_launch
 
 
-DOMINANT_KERNEL = "ffn_block_kernel"
+DOMINANT_KERNEL = "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"
 
 
 def _time_fused(e, items, gran, run, reps: int) -> float:
@@ -82,12 +87,12 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
     return tot / (reps * len(items))
 
 
-PMC_FILE = "r03_pmc_ffnblk_fetch.json"
+PMC_FILE = "r03_pmc_fc1_fetch.json"
 
 
 def pmc_traffic():
     """HBM bytes per launch of the dominant kernel from the committed FETCH_SIZE pass of THIS kernel
-    (tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py ffnblk, x2 gfx950
+    (tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950
     correction; a counter pass serialises dispatches, so it is not repeated inside the timed run). None
     when the profile is absent or measured another kernel."""
     path = os.path.join(REPO, "profiles", PMC_FILE)
@@ -726,8 +731,8 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "ffn_block_kernel (out_proj + residual + LayerNorm + fc1 + SwiGLU, 75.5 MB bf16 "
-                                   "weights per launch)",
+            "roofline": {"kernel": "gemv_kernel<2, 4, 8, 16, 1, 3, 1> (fc1: LayerNorm prologue + packed SwiGLU "
+                                   "epilogue, 67.1 MB bf16 weights per launch)",
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2, bytes/launch)",

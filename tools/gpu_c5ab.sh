@@ -1,5 +1,4 @@
-# C2 step A/B (ffn_block at 2 rows), then the C5 share at full length with the default plan
+# C2 step A/B: prefetch role sizes with the separate out_proj / fc1 launches
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 200 python -u tools/step_ab.py '[{"ffn_block": false}, {"ffn_block": true}, {"ffn_block": false}, {"ffn_block": true}]' > gpurun_out/ffn2_ab.jsonl 2>gpurun_out/ffn2_ab.err || exit $?
-timeout -k 10 200 python -u tools/bench_c5.py > gpurun_out/c5_full.jsonl 2>gpurun_out/c5_full.err || exit $?
+timeout -k 10 400 python -u tools/step_ab.py '[{"prefetch_blocks": 256, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 4}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 16}, {"prefetch_blocks": 384, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 512, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 512, "prefetch_fc1_mb": 16}, {"prefetch_blocks": 128, "prefetch_fc1_mb": 4}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 8}]' > gpurun_out/pf_ab3.jsonl 2>gpurun_out/pf_ab3.err || exit $?

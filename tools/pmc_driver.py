@@ -34,8 +34,11 @@ def main(which: str, reps: int = 2):
         e.vc.normal_()
     e.stream.synchronize()
     e.pos_hi[0] = POS
-    if which == "fc1":  # the standalone fc1 GEMV (the C2 step runs it inside zmi_ffn_block)
+    if which == "fc1":  # the fc1 GEMV as the C2 step runs it (its own launch)
         e.ffn_block = False
+        e._build_plan()
+    if which == "ffnblk":  # the fused out_proj + fc1 launch (off by default)
+        e.ffn_block = True
         e._build_plan()
     plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
     for _ in range(reps):

@@ -1,8 +1,7 @@
 #!/bin/bash
 # GPU-box profiling pass for this round (run from the repo root on the box):
 #  1. kernel stats of the default bench (rocprofv3 --kernel-trace --stats);
-#  2. HBM-traffic counter passes, one counter per pass: FETCH_SIZE on the fused out_proj + fc1 launch and the
-#     standalone fc1 GEMV, FETCH_SIZE and
+#  2. HBM-traffic counter passes, one counter per pass: FETCH_SIZE on the fc1 GEMV, FETCH_SIZE and
 #     WRITE_SIZE on the attention kernel (tools/pmc_driver.py);
 #  3. MFMA-busy pass over the DAC decode.
 # Everything kept lands in gpurun_out/keep/ (copied into profiles/ afterwards).
@@ -21,7 +20,6 @@ pmc() {  # counter, driver, kernel substring, algorithmic bytes, tag
   f=$(find gpurun_out/pmc_$5 -name "*counter_collection.csv" -print -quit)
   python tools/pmc_summary.py "$f" "$3" $4 > $K/pmc_$5.json && rm -rf gpurun_out/pmc_$5
 }
-pmc FETCH_SIZE ffnblk ffn_block_kernel 75497472 ffnblk_fetch || exit $?
 pmc FETCH_SIZE fc1 "gemv_kernel<2, 4, 8, 16, 1, 3, 1>" 67158016 fc1_fetch || exit $?
 pmc FETCH_SIZE attnblk attn_block_kernel 15007744 attnblk_fetch || exit $?
 pmc WRITE_SIZE attnblk attn_block_kernel 15007744 attnblk_write || exit $?

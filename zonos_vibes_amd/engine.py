@@ -107,16 +107,19 @@ class HipEngine:
         self.attn_forms = ("split", "xs")
         self.attn_self_slices = 8
         # prefetch-only workgroups in that launch warm the Infinity Cache with out_proj's weights and the
-        # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only)
-        self.prefetch_blocks = 192
-        self.prefetch_fc1_mb = 0  # measured: fc1 bytes outlast the attention window (tools/step_ab.py)
+        # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only). With out_proj and fc1 as
+        # separate launches: C2 step 971 us (192 blocks, out_proj only), 959 (192, + 8 MB of fc1), 944-947
+        # (256, + 4-8 MB), 966 (256, + 16 MB), 974 (512, + 8 MB) (profiles/r03_prefetch_ab.jsonl)
+        self.prefetch_blocks = 256
+        self.prefetch_fc1_mb = 8
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
         # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
-        # device: fc1's weights stream while the out_proj chain runs (identical bits). Above 2 rows the launch
-        # loses to the separate ones (every workgroup DMAs all rows and gathers all rows' residual granules):
-        # C5-shaped steps at 4 / 8 / 16 rows 1.21 / 1.52 / 2.06 ms without it against 1.26 / 1.61 / 2.27 with it
-        # (tools/bench_c5.py, profiles/r03_ffnblk_rows_ab.jsonl)
-        self.ffn_block = True
+        # device: fc1's weights stream while the out_proj chain runs (identical bits). Off: it loses to the
+        # separate launches at every row count measured (C2 step 972 us without it against 983 with it,
+        # profiles/r03_ffnblk_c2_ab.jsonl; C5-shaped steps at 4 / 8 / 16 rows 1.21 / 1.52 / 2.06 ms against
+        # 1.26 / 1.61 / 2.27, profiles/r03_ffnblk_rows_ab.jsonl: every workgroup DMAs all rows and gathers all
+        # rows' residual granules, and the separate out_proj finds its weights prefetched by the attention block)
+        self.ffn_block = False
         self.ffn_block_rows = 2
         # attention + out_proj + fc1 as ONE launch after a plain QKV launch (zmi_attn_ffn_block) for <= 2 rows
         # (batch 1) at positions < 1024: out_proj's and fc1's weights stream under the attention chain

@@ -89,6 +89,7 @@ class HybridEngine(HipEngine):
         # prefetch the layer's out_proj weights into the Infinity Cache during the step phase: measured slower
         # (C4 300 frames: 320 ms off; 321, 333 and 361 ms with 64, 192 and 32 prefetch workgroups), so off
         self.mamba_prefetch = False
+        self.prefetch_blocks, self.prefetch_fc1_mb = 192, 0  # the MHA blocks' out_proj prefetch (measured in round 2)
 
     def _kv_layers(self) -> int:
         return len(self.attn_idx)
