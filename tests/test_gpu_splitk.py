@@ -1,0 +1,40 @@
+"""The split-K fc2 GEMM (zmi_gemv_splitk: one workgroup per 64-column block and 1024-element K segment, fp32
+segment sums, a reduce launch adding them in K order + the residual epilogue) against zmi_gemv_launch's GEMV
+for the same K = 8192 EPI_RESIDUAL op: bit-identical for row counts on and off the 16-row tile (a row's result
+may not depend on the batch it is computed in)."""
+import ctypes
+
+import pytest
+import torch
+
+from tests.test_gpu_kernels import DEV, _lib, pack, rnd, stream_ptr
+
+pytestmark = pytest.mark.gpu
+
+D, F = 2048, 8192
+
+
+@pytest.mark.parametrize("M", [1, 16, 17, 64, 128, 322])
+def test_splitk_fc2_bit_identical_to_gemv(M):
+    L = _lib()
+    W = rnd(D, F, scale=0.03, seed=70)
+    Wp = pack(W)[0]
+    h = rnd(M, F, scale=1.0, seed=71)
+    x0 = rnd(M, D, scale=2.0, seed=72)
+
+    def args(out):
+        a = L.GemvArgs()
+        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, F, F
+        a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), D, D, 1e-5
+        return a
+
+    ref = x0.clone()
+    a = args(ref)
+    L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), L.EPI_RESIDUAL, stream_ptr()))
+    got = x0.clone()
+    nf = L.lib().zmi_gemv_splitk_floats(M, D)
+    part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
+    a = args(got)
+    L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, stream_ptr()), "splitk")
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()

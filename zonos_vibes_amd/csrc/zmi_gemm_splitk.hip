@@ -1,0 +1,126 @@
+// Many-row fc2 (reference zonos/backbone/_torch.py:152, x = x + fc2(...) at :101) as a split-K GEMM: one
+// workgroup per (64-column block, 1024-element K segment), then a reduce launch that sums the 8 segments in
+// order and applies the residual epilogue.
+//
+// Why: the GEMV form (zmi_gemv_impl.h, W = 8 waves each owning one K segment of a column group) re-reads the
+// whole activation block [M][8192] once per column group; at 128 rows (C3's 64 slots) that is 2 MB per
+// workgroup, 256 MB of L2 -> LDS traffic per launch, and the launch took 37 us for 33.6 MB of weights. Here
+// a workgroup reads only its K segment of the rows (256 KB at 128 rows; 64 MB per launch), its 64 columns'
+// weights for that segment once (128 KB, in registers), and keeps the GEMV's arithmetic: per wave (one 8-column
+// group) and row tile of 16 rows, the MFMA chain over the segment's 16 chunks of 64 (k-half 0 and k-half 1 in
+// two accumulators, summed with the same DPP move), stored as that segment's fp32 sum; the reduce adds the
+// segments in K order (the GEMV's wave order) and applies x = bf16(x + bf16(sum)). A row's result is
+// bit-identical to zmi_gemv_launch's for any M (tested).
+#include <algorithm>
+
+#include "zmi_common.h"
+#include "zmi_kernels.h"
+#include "zmi_gemv_impl.h"
+
+namespace {
+
+using zmi_gemv::dma_piece;
+using zmi_gemv::ror8;
+
+constexpr int K = 8192, NSEG = 8, NL = 16, KS = K / NSEG;  // 1024 K per segment = 16 chunks of 64
+constexpr int KC = K / 64;
+constexpr int NWV = 8, NT = NWV * 64;                       // wave g = column group cb * 8 + g
+constexpr int RT = 16;                                      // rows per tile (one MFMA tile)
+constexpr int SROW = KS + 8;                                // LDS row stride (bf16): bank-spread A reads
+constexpr int TILE_BYTES = RT * SROW * 2;
+constexpr int PIECES = RT * KS / 512;                       // 1 KiB DMA pieces per tile (32)
+
+__global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  const int seg = b / n_cb, cb = b - seg * n_cb;  // consecutive blocks: one segment, neighbouring columns
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = cb * NWV + wave;
+  const int M = a.M, N = a.N;
+  const int n_rt = (M + RT - 1) / RT;
+  bf16_t* tiles = reinterpret_cast<bf16_t*>(smem);  // two tile buffers
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)seg * KS;
+
+  auto stage = [&](int rt, int buf) {  // the tile's rows of this segment, 1 KiB pieces spread over the waves
+    const int row0 = rt * RT, rows = min(RT, M - row0);
+    bf16_t* dst = tiles + (size_t)buf * (TILE_BYTES / 2);
+    for (int pc = wave; pc < rows * (KS / 512); pc += NWV) {
+      const int r = pc / (KS / 512), p = pc - r * (KS / 512);
+      dma_piece(X + (size_t)(row0 + r) * a.ldx + p * 512 + lane * 8, dst + r * SROW + p * 512);
+    }
+  };
+  stage(0, 0);
+  // the wave's weights for this segment: group g, chunks seg * 16 .. + 15 (layout M8), all in flight
+  const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)g * KC + seg * NL) * 1024;
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wbase), (short)0, NL * 1024, 0x00020000);
+  u32x4_t wf[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, 2);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // the first tile's pieces (issued before)
+  for (int rt = 0; rt < n_rt; ++rt) {
+    __syncthreads();  // tile rt landed for every wave's pieces; buffer rt + 1 is free
+    if (rt + 1 < n_rt) stage(rt + 1, (rt + 1) & 1);
+    const int row0 = rt * RT, rows = min(RT, M - row0);
+    const bf16_t* xs = tiles + (size_t)(rt & 1) * (TILE_BYTES / 2);
+    f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const int ar = min(lane & 15, rows - 1);
+    const bf16_t* xa = xs + ar * SROW + (lane >> 4) * 8;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const uint4 x0 = *reinterpret_cast<const uint4*>(xa + j * 64);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(xa + j * 64 + 32);
+      const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[j]);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), wv, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), wv, acc1, 0, 0, 0);
+    }
+    // segment sum = k-half 0 (tile columns 0..7) + k-half 1 (columns 8..15 moved down): element q of lane l
+    // is row 4 (l >> 4) + q, column l & 15
+    const int c = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = acc0[q] + ror8(acc1[q]);
+      if (c < 8 && rb + q < rows) part[((size_t)seg * M + row0 + rb + q) * N + g * 8 + c] = v;
+    }
+    if (rt + 1 < n_rt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces
+  }
+}
+
+// x[m][n] = bf16(x + bf16(sum over segments 0..7 in order)), the GEMV's EPI_RESIDUAL epilogue
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int M, int N, bf16_t* out, int ldo) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * N) return;
+  const size_t m = i / N, n = i - m * N;
+  float v = part[i];
+#pragma unroll
+  for (int s = 1; s < NSEG; ++s) v += part[(size_t)s * M * N + i];
+  bf16_t* o = out + m * ldo + n;
+  *o = (bf16_t)f2bf(bf2f(*o) + bfround(v));
+}
+
+}  // namespace
+
+extern "C" int64_t zmi_gemv_splitk_floats(int M, int N) { return M <= 0 || N <= 0 ? -1 : (int64_t)NSEG * M * N; }
+
+extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream) {
+  const ZmiGemvArgs& a = *args;
+  if (epi != ZMI_EPI_RESIDUAL) return zmi_fail_msg("gemv_splitk: EPI_RESIDUAL only");
+  if (a.K != K || a.ln_w || a.pro != ZMI_PRO_AUTO) return zmi_fail_msg("gemv_splitk: plain K = 8192 only (fc2)");
+  if (a.N % (8 * NWV) || a.n_valid != a.N) return zmi_fail_msg("gemv_splitk: N a multiple of 64, unpadded");
+  if (a.M < 1 || a.ldx % 8 || a.ldo < a.N) return zmi_fail_msg("gemv_splitk: rows / strides");
+  if (!part || part_floats < (int64_t)NSEG * a.M * a.N) return zmi_fail_msg("gemv_splitk: partial buffer too small");
+  const int n_cb = a.N / (8 * NWV);
+  const size_t lds = 2 * (size_t)TILE_BYTES;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  ZMI_CHECK(attr);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(splitk_kernel, dim3(n_cb * NSEG), dim3(NT), lds, s, a, part, n_cb);
+  ZMI_CHECK(hipGetLastError());
+  const size_t total = (size_t)a.M * a.N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M, a.N,
+                     (bf16_t*)a.out, a.ldo);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}

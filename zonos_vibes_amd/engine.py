@@ -127,6 +127,9 @@ class HipEngine:
         # hand-off of the chain takes 3-5 us under the weight stream against ~1.5 on an idle memory system,
         # DESIGN.md §5)
         self.attn_ffn = False
+        # fc2 over >= `splitk_rows` rows as a split-K GEMM (zmi_gemv_splitk: each column block reads the
+        # activation rows once; identical bits); 0 = never
+        self.splitk_rows = 16
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
@@ -173,6 +176,8 @@ class HipEngine:
             self.ffn_gran = z(self.L, R, self.lib.zmi_ffn_block_gran_words(1), dt=torch.int64)
             # zmi_attn_ffn_block hand-off granules (the attention output rows), one area per layer
             self.attn_gran = z(self.L, R, self.lib.zmi_attn_ffn_gran_words(1), dt=torch.int64)
+            # zmi_gemv_splitk's fp32 segment sums (fc2 over many rows: decode and prefill)
+            self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, 2 * self.max_prefill), d), dt=torch.float32)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -267,7 +272,16 @@ class HipEngine:
 
     def _run_gemv(self, item):
         a, epi = item
+        if self._use_splitk(a, epi):
+            _lib.check(self.lib.zmi_gemv_splitk(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
+                                                self.splitk_part.numel(), self.sptr), "gemv_splitk")
+            return
         _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
+
+    def _use_splitk(self, a, epi) -> bool:
+        return (self.splitk_rows > 0 and a.M >= self.splitk_rows and a.K == 8192 and epi == _lib.EPI_RESIDUAL
+                and not a.ln_w and a.N % 64 == 0 and a.n_valid == a.N
+                and a.M * a.N * 8 <= self.splitk_part.numel())
 
     def _build_plan(self):
         """Invalidate the per-row-count decode plans and graphs (new weights or buffers)."""
