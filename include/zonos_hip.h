@@ -76,6 +76,10 @@ int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
  * order); reads the activation rows once per column block instead of once per column group. part:
  * zmi_gemv_splitk_floats(M, N) floats. */
 int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream);
+/* The same with ln_w != NULL (N = 2048): the reduce also writes LayerNorm(new row; ln_w, ln_b, eps) to xn [M][ldxn],
+ * bit-identical to zmi_layernorm_rows of the new rows, so the next op's LayerNorm pre-pass is not launched. */
+int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, const void* ln_w,
+                       const void* ln_b, float eps, void* xn, int ldxn, void* stream);
 int64_t zmi_gemv_splitk_floats(int M, int N);
 /* out[r] = LayerNorm(x[r]) bf16, r < m (nn.LayerNorm, _torch.py:62: norm_f for the backbone plugin),
  * with the GEMV LayerNorm prologue's arithmetic; k in {512, 1024, 2048, 4096}. */

@@ -38,3 +38,38 @@ def test_splitk_fc2_bit_identical_to_gemv(M):
     L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, stream_ptr()), "splitk")
     torch.cuda.synchronize()
     assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
+
+
+@pytest.mark.parametrize("M", [16, 33, 128])
+def test_splitk_fused_layernorm_bit_identical(M):
+    """zmi_gemv_splitk_ln: the reduce also writes LayerNorm(new rows) -- equal to the GEMV followed by
+    zmi_layernorm_rows (the next op's pre-pass it replaces)."""
+    L = _lib()
+    W = rnd(D, F, scale=0.03, seed=73)
+    Wp = pack(W)[0]
+    h = rnd(M, F, scale=1.0, seed=74)
+    x0 = rnd(M, D, scale=2.0, seed=75)
+    lw, lb = (rnd(D, scale=0.1, seed=76) + 1).contiguous(), rnd(D, scale=0.02, seed=77)
+
+    def args(out):
+        a = L.GemvArgs()
+        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, F, F
+        a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), D, D, 1e-5
+        return a
+
+    ref = x0.clone()
+    a = args(ref)
+    L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), L.EPI_RESIDUAL, stream_ptr()))
+    ref_n = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    L.check(L.lib().zmi_layernorm_rows(ref.data_ptr(), D, M, D, lw.data_ptr(), lb.data_ptr(), 1e-5, ref_n.data_ptr(), D,
+                                       stream_ptr()))
+    got = x0.clone()
+    got_n = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    nf = L.lib().zmi_gemv_splitk_floats(M, D)
+    part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
+    a = args(got)
+    L.check(L.lib().zmi_gemv_splitk_ln(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, lw.data_ptr(), lb.data_ptr(),
+                                       1e-5, got_n.data_ptr(), D, stream_ptr()), "splitk_ln")
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(got_n, ref_n), (got_n != ref_n).nonzero()[:4].tolist()

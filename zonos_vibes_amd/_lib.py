@@ -103,6 +103,8 @@ _SIGS = {
     "zmi_ffn_block_gran_words": (c_int64, [c_int]),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
+    "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,
+                                   c_void_p, c_int, c_void_p]),
     "zmi_attn_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs),
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "zmi_attn_ffn_gran_words": (c_int64, [c_int]),

@@ -99,12 +99,63 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
   *o = (bf16_t)f2bf(bf2f(*o) + bfround(v));
 }
 
+// The same reduce + residual for rows of 2048 columns, then the LayerNorm of each new row into `xn` (the next
+// op's prologue, zmi_layernorm_rows' arithmetic: part q = wave q, lane L's chunk at q 512 + 8 L, parts combined
+// (p0 + p1) + (p2 + p3), two passes): one 4-wave workgroup per row, so the next layer's LayerNorm pre-pass launch
+// is not needed.
+__global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(const float* part, int M, bf16_t* out, int ldo,
+                                                               const bf16_t* lw, const bf16_t* lb, float eps,
+                                                               bf16_t* xn, int ldn) {
+  constexpr int N = 2048, NQ = ln_parts(N);
+  static_assert(NQ == 4, "one wave per LayerNorm part");
+  __shared__ float ps[2][NQ];
+  const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, q = t >> 6;
+  const int e0 = q * 512 + lane * 8;
+  bf16_t* orow = out + (size_t)m * ldo;
+  const uint4 xv = *reinterpret_cast<const uint4*>(orow + e0);
+  const uint4 gw = *reinterpret_cast<const uint4*>(lw + e0), gb = *reinterpret_cast<const uint4*>(lb + e0);
+  float4 pv[NSEG][2];
+#pragma unroll
+  for (int s = 0; s < NSEG; ++s) {
+    const float* pr = part + ((size_t)s * M + m) * N + e0;
+    pv[s][0] = *reinterpret_cast<const float4*>(pr);
+    pv[s][1] = *reinterpret_cast<const float4*>(pr + 4);
+  }
+  const uint32_t xu[4] = {xv.x, xv.y, xv.z, xv.w};
+  uint32_t nu[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v0 = j < 2 ? (j == 0 ? pv[0][0].x : pv[0][0].z) : (j == 2 ? pv[0][1].x : pv[0][1].z);
+    float v1 = j < 2 ? (j == 0 ? pv[0][0].y : pv[0][0].w) : (j == 2 ? pv[0][1].y : pv[0][1].w);
+#pragma unroll
+    for (int s = 1; s < NSEG; ++s) {
+      v0 += j < 2 ? (j == 0 ? pv[s][0].x : pv[s][0].z) : (j == 2 ? pv[s][1].x : pv[s][1].z);
+      v1 += j < 2 ? (j == 0 ? pv[s][0].y : pv[s][0].w) : (j == 2 ? pv[s][1].y : pv[s][1].w);
+    }
+    nu[j] = f2bf(bf2f(xu[j]) + bfround(v0)) | (f2bf(bf2f(xu[j] >> 16) + bfround(v1)) << 16);
+  }
+  const uint4 nx = uint4{nu[0], nu[1], nu[2], nu[3]};
+  *reinterpret_cast<uint4*>(orow + e0) = nx;
+  const float s1 = wave_sum(ln_chunk_sum(nx, 0.f, false));
+  if (lane == 0) ps[0][q] = s1;
+  __syncthreads();
+  const float mean = ln_combine<NQ>(ps[0]) / (float)N;
+  const float s2 = wave_sum(ln_chunk_sum(nx, mean, true));
+  if (lane == 0) ps[1][q] = s2;
+  __syncthreads();
+  const float rstd = 1.0f / sqrtf(ln_combine<NQ>(ps[1]) / (float)N + eps), nbias = -mean * rstd;
+  *reinterpret_cast<uint4*>(xn + (size_t)m * ldn + e0) = ln_apply(nx, gw, gb, rstd, nbias);
+}
+
 }  // namespace
 
 extern "C" int64_t zmi_gemv_splitk_floats(int M, int N) { return M <= 0 || N <= 0 ? -1 : (int64_t)NSEG * M * N; }
 
-extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream) {
+extern "C" int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, const void* ln_w,
+                                  const void* ln_b, float eps, void* xn, int ldxn, void* stream) {
   const ZmiGemvArgs& a = *args;
+  if (ln_w && (!ln_b || !xn || a.N != 2048 || ldxn < 2048 || ldxn % 8 || a.ldo % 8))
+    return zmi_fail_msg("gemv_splitk_ln: the fused LayerNorm needs N = 2048, ln_b, xn (ldxn % 8) and ldo % 8");
   if (epi != ZMI_EPI_RESIDUAL) return zmi_fail_msg("gemv_splitk: EPI_RESIDUAL only");
   if (a.K != K || a.ln_w || a.pro != ZMI_PRO_AUTO) return zmi_fail_msg("gemv_splitk: plain K = 8192 only (fc2)");
   if (a.N % (8 * NWV) || a.n_valid != a.N) return zmi_fail_msg("gemv_splitk: N a multiple of 64, unpadded");
@@ -118,9 +169,18 @@ extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, in
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(splitk_kernel, dim3(n_cb * NSEG), dim3(NT), lds, s, a, part, n_cb);
   ZMI_CHECK(hipGetLastError());
-  const size_t total = (size_t)a.M * a.N;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M, a.N,
-                     (bf16_t*)a.out, a.ldo);
+  if (ln_w) {
+    hipLaunchKernelGGL(splitk_reduce_ln_kernel, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,
+                       (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, (bf16_t*)xn, ldxn);
+  } else {
+    const size_t total = (size_t)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M, a.N,
+                       (bf16_t*)a.out, a.ldo);
+  }
   ZMI_CHECK(hipGetLastError());
   return 0;
+}
+
+extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream) {
+  return zmi_gemv_splitk_ln(args, epi, part, part_floats, nullptr, nullptr, 0.f, nullptr, 0, stream);
 }

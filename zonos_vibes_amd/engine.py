@@ -348,11 +348,15 @@ class HipEngine:
             # zmi_layernorm_rows gives the prologue's bits, so the plan may switch at any row count
             pre = rows > 4
             plan = []
+            ln_ready = [False]  # the previous split-K fc2 already wrote the LayerNorm'd rows to xn
 
             def normed(ln):
                 """(activation rows, prologue LayerNorm) of a LayerNorm'd GEMV, with the pre-pass item."""
                 if not pre:
                     return self.x, ln
+                if ln_ready[0]:
+                    ln_ready[0] = False
+                    return self.xn, None
                 plan.append(("call", lambda ln=ln: _lib.check(self.lib.zmi_layernorm_rows(
                     self.x.data_ptr(), d, rows, d, ln[0].data_ptr(), ln[1].data_ptr(), self.eps, self.xn.data_ptr(),
                     d, self.sptr), "ln")))
@@ -399,7 +403,15 @@ class HipEngine:
                     xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
                     plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
                                                     self.F, ln=ln)))
-                plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
+                fc2 = self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)
+                last = i + 1 == len(w["layers"])
+                nxt = (w["nf_w"], w["nf_b"]) if last else (w["layers"][i + 1]["ln1_w"], w["layers"][i + 1]["ln1_b"])
+                if pre and (last or not fused) and self._use_splitk(*fc2) and d == 2048:
+                    # the split-K reduce also writes LayerNorm(new x) for the next op (no pre-pass launch)
+                    plan.append(("splitkln", (fc2, nxt)))
+                    ln_ready[0] = True
+                else:
+                    plan.append(("gemv", fc2))
             xin, ln = normed((w["nf_w"], w["nf_b"]))
             heads = self._gemv(w["heads"], xin, rows, HEADS_N_PAD, d, _lib.EPI_LOGITS, self.logits, 0,
                                n_valid=HEADS_N, ln=ln)
@@ -504,6 +516,11 @@ class HipEngine:
                 self._run_ffn_block(item)
             elif kind == "attnffn":
                 self._run_attn_ffn(item)
+            elif kind == "splitkln":
+                (a, epi), ln = item
+                _lib.check(self.lib.zmi_gemv_splitk_ln(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
+                                                       self.splitk_part.numel(), ln[0].data_ptr(), ln[1].data_ptr(),
+                                                       self.eps, self.xn.data_ptr(), self.d, self.sptr), "gemv_splitk_ln")
             elif kind == "attn":
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
                 self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
