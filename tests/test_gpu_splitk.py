@@ -1,7 +1,8 @@
-"""The split-K fc2 GEMM (zmi_gemv_splitk: one workgroup per 64-column block and 1024-element K segment, fp32
-segment sums, a reduce launch adding them in K order + the residual epilogue) against zmi_gemv_launch's GEMV
-for the same K = 8192 EPI_RESIDUAL op: bit-identical for row counts on and off the 16-row tile (a row's result
-may not depend on the batch it is computed in)."""
+"""The split-K fc2 / out_proj GEMM (zmi_gemv_splitk: one workgroup per 64-column block and K segment -- 8 x 1024
+for K = 8192, 4 x 512 for K = 2048 --, fp32 segment sums, a reduce launch adding them in K order + the residual
+epilogue) against zmi_gemv_launch's GEMV for the same EPI_RESIDUAL op: bit-identical for row counts on and off
+the 16-row tile and across the GEMV's own launch forms at those counts (a row's result may not depend on the
+batch it is computed in)."""
 import ctypes
 
 import pytest
@@ -14,17 +15,18 @@ pytestmark = pytest.mark.gpu
 D, F = 2048, 8192
 
 
-@pytest.mark.parametrize("M", [1, 16, 17, 64, 128, 322])
-def test_splitk_fc2_bit_identical_to_gemv(M):
+@pytest.mark.parametrize("K", [F, D])
+@pytest.mark.parametrize("M", [1, 16, 17, 64, 65, 128, 322])
+def test_splitk_bit_identical_to_gemv(M, K):
     L = _lib()
-    W = rnd(D, F, scale=0.03, seed=70)
+    W = rnd(D, K, scale=0.03, seed=70)
     Wp = pack(W)[0]
-    h = rnd(M, F, scale=1.0, seed=71)
+    h = rnd(M, K, scale=1.0, seed=71)
     x0 = rnd(M, D, scale=2.0, seed=72)
 
     def args(out):
         a = L.GemvArgs()
-        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, F, F
+        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, K, K
         a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), D, D, 1e-5
         return a
 
@@ -40,20 +42,21 @@ def test_splitk_fc2_bit_identical_to_gemv(M):
     assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
 
 
+@pytest.mark.parametrize("K", [F, D])
 @pytest.mark.parametrize("M", [16, 33, 128])
-def test_splitk_fused_layernorm_bit_identical(M):
+def test_splitk_fused_layernorm_bit_identical(M, K):
     """zmi_gemv_splitk_ln: the reduce also writes LayerNorm(new rows) -- equal to the GEMV followed by
     zmi_layernorm_rows (the next op's pre-pass it replaces)."""
     L = _lib()
-    W = rnd(D, F, scale=0.03, seed=73)
+    W = rnd(D, K, scale=0.03, seed=73)
     Wp = pack(W)[0]
-    h = rnd(M, F, scale=1.0, seed=74)
+    h = rnd(M, K, scale=1.0, seed=74)
     x0 = rnd(M, D, scale=2.0, seed=75)
     lw, lb = (rnd(D, scale=0.1, seed=76) + 1).contiguous(), rnd(D, scale=0.02, seed=77)
 
     def args(out):
         a = L.GemvArgs()
-        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, F, F
+        a.W, a.X, a.M, a.N, a.K, a.ldx = Wp.data_ptr(), h.data_ptr(), M, D, K, K
         a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), D, D, 1e-5
         return a
 

@@ -1,6 +1,8 @@
 """The bench's C3-shaped batch sample (64 mixed-length utterances through 64 slots) under a profiler.
 
-    rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o bprof -- python tools/bench_batch.py
+    rocprofv3 --kernel-trace --stats -d gpurun_out/bprof -o bprof -- python tools/bench_batch.py ['{"knob": v}']
+
+An optional JSON argument sets engine attributes first (A/B runs).
 """
 import json
 import os
@@ -18,7 +20,11 @@ def main():
     dev = torch.device("cuda", 0)
     m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=bench.LC + bench.N_NEW + 9,
                         max_prefill=bench.LC + 1)
-    print(json.dumps(bench.time_batch(m, dev)), flush=True)
+    opts = json.loads(sys.argv[1]) if len(sys.argv) > 1 else {}
+    for k, v in opts.items():
+        setattr(m.engine, k, v)
+    m.engine._build_plan()
+    print(json.dumps(dict(bench.time_batch(m, dev), opts=opts)), flush=True)
 
 
 if __name__ == "__main__":

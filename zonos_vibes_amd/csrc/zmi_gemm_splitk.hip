@@ -1,6 +1,7 @@
-// Many-row fc2 (reference zonos/backbone/_torch.py:152, x = x + fc2(...) at :101) as a split-K GEMM: one
-// workgroup per (64-column block, 1024-element K segment), then a reduce launch that sums the 8 segments in
-// order and applies the residual epilogue.
+// Many-row fc2 and out_proj (reference zonos/backbone/_torch.py:152 and :140, x = x + ... at :100-101) as
+// split-K GEMMs: one workgroup per (64-column block, K segment of the GEMV's wave split: fc2 8 x 1024, out_proj
+// 4 x 512), then a reduce launch that sums the segments in order and applies the residual epilogue (optionally
+// also the next op's LayerNorm).
 //
 // Why: the GEMV form (zmi_gemv_impl.h, W = 8 waves each owning one K segment of a column group) re-reads the
 // whole activation block [M][8192] once per column group; at 128 rows (C3's 64 slots) that is 2 MB per
@@ -22,15 +23,20 @@ namespace {
 using zmi_gemv::dma_piece;
 using zmi_gemv::ror8;
 
-constexpr int K = 8192, NSEG = 8, NL = 16, KS = K / NSEG;  // 1024 K per segment = 16 chunks of 64
-constexpr int KC = K / 64;
-constexpr int NWV = 8, NT = NWV * 64;                       // wave g = column group cb * 8 + g
-constexpr int RT = 16;                                      // rows per tile (one MFMA tile)
-constexpr int SROW = KS + 8;                                // LDS row stride (bf16): bank-spread A reads
-constexpr int TILE_BYTES = RT * SROW * 2;
-constexpr int PIECES = RT * KS / 512;                       // 1 KiB DMA pieces per tile (32)
+// K segments are the GEMV's wave segments: K = 8192 (fc2) W = 8 x 16 chunks, K = 2048 (out_proj) W = 4 x 8
+template <int K>
+struct Shape {
+  static constexpr int NSEG = K == 8192 ? 8 : 4, KS = K / NSEG, NL = KS / 64, KC = K / 64;
+  static constexpr int SROW = KS + 8;  // LDS row stride (bf16): bank-spread A reads
+  static constexpr int TILE_BYTES = 16 * SROW * 2;
+};
+constexpr int NWV = 8, NT = NWV * 64;  // wave g = column group cb * 8 + g
+constexpr int RT = 16;                 // rows per tile (one MFMA tile)
 
+template <int K>
 __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb) {
+  using S = Shape<K>;
+  constexpr int NSEG = S::NSEG, KS = S::KS, NL = S::NL, KC = S::KC, SROW = S::SROW, TILE_BYTES = S::TILE_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int seg = b / n_cb, cb = b - seg * n_cb;  // consecutive blocks: one segment, neighbouring columns
@@ -87,7 +93,8 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
   }
 }
 
-// x[m][n] = bf16(x + bf16(sum over segments 0..7 in order)), the GEMV's EPI_RESIDUAL epilogue
+// x[m][n] = bf16(x + bf16(sum over the segments in order)), the GEMV's EPI_RESIDUAL epilogue
+template <int NSEG>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int M, int N, bf16_t* out, int ldo) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (size_t)M * N) return;
@@ -103,6 +110,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
 // op's prologue, zmi_layernorm_rows' arithmetic: part q = wave q, lane L's chunk at q 512 + 8 L, parts combined
 // (p0 + p1) + (p2 + p3), two passes): one 4-wave workgroup per row, so the next layer's LayerNorm pre-pass launch
 // is not needed.
+template <int NSEG>
 __global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(const float* part, int M, bf16_t* out, int ldo,
                                                                const bf16_t* lw, const bf16_t* lb, float eps,
                                                                bf16_t* xn, int ldn) {
@@ -149,7 +157,32 @@ __global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(const float* part
 
 }  // namespace
 
-extern "C" int64_t zmi_gemv_splitk_floats(int M, int N) { return M <= 0 || N <= 0 ? -1 : (int64_t)NSEG * M * N; }
+extern "C" int64_t zmi_gemv_splitk_floats(int M, int N) { return M <= 0 || N <= 0 ? -1 : (int64_t)8 * M * N; }
+
+namespace {
+template <int K>
+int launch_splitk(const ZmiGemvArgs& a, float* part, const void* ln_w, const void* ln_b, float eps, void* xn, int ldxn,
+                  hipStream_t s) {
+  using S = Shape<K>;
+  const int n_cb = a.N / (8 * NWV);
+  const size_t lds = 2 * (size_t)S::TILE_BYTES;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  ZMI_CHECK(attr);
+  hipLaunchKernelGGL(splitk_kernel<K>, dim3(n_cb * S::NSEG), dim3(NT), lds, s, a, part, n_cb);
+  ZMI_CHECK(hipGetLastError());
+  if (ln_w) {
+    hipLaunchKernelGGL(splitk_reduce_ln_kernel<S::NSEG>, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,
+                       (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, (bf16_t*)xn, ldxn);
+  } else {
+    const size_t total = (size_t)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel<S::NSEG>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M,
+                       a.N, (bf16_t*)a.out, a.ldo);
+  }
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+}  // namespace
 
 extern "C" int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, const void* ln_w,
                                   const void* ln_b, float eps, void* xn, int ldxn, void* stream) {
@@ -157,28 +190,15 @@ extern "C" int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part,
   if (ln_w && (!ln_b || !xn || a.N != 2048 || ldxn < 2048 || ldxn % 8 || a.ldo % 8))
     return zmi_fail_msg("gemv_splitk_ln: the fused LayerNorm needs N = 2048, ln_b, xn (ldxn % 8) and ldo % 8");
   if (epi != ZMI_EPI_RESIDUAL) return zmi_fail_msg("gemv_splitk: EPI_RESIDUAL only");
-  if (a.K != K || a.ln_w || a.pro != ZMI_PRO_AUTO) return zmi_fail_msg("gemv_splitk: plain K = 8192 only (fc2)");
+  if ((a.K != 8192 && a.K != 2048) || a.ln_w || a.pro != ZMI_PRO_AUTO)
+    return zmi_fail_msg("gemv_splitk: plain K = 8192 (fc2) or 2048 (out_proj) only");
   if (a.N % (8 * NWV) || a.n_valid != a.N) return zmi_fail_msg("gemv_splitk: N a multiple of 64, unpadded");
   if (a.M < 1 || a.ldx % 8 || a.ldo < a.N) return zmi_fail_msg("gemv_splitk: rows / strides");
-  if (!part || part_floats < (int64_t)NSEG * a.M * a.N) return zmi_fail_msg("gemv_splitk: partial buffer too small");
-  const int n_cb = a.N / (8 * NWV);
-  const size_t lds = 2 * (size_t)TILE_BYTES;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  ZMI_CHECK(attr);
+  const int nseg = a.K == 8192 ? Shape<8192>::NSEG : Shape<2048>::NSEG;
+  if (!part || part_floats < (int64_t)nseg * a.M * a.N) return zmi_fail_msg("gemv_splitk: partial buffer too small");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(splitk_kernel, dim3(n_cb * NSEG), dim3(NT), lds, s, a, part, n_cb);
-  ZMI_CHECK(hipGetLastError());
-  if (ln_w) {
-    hipLaunchKernelGGL(splitk_reduce_ln_kernel, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,
-                       (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, (bf16_t*)xn, ldxn);
-  } else {
-    const size_t total = (size_t)a.M * a.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M, a.N,
-                       (bf16_t*)a.out, a.ldo);
-  }
-  ZMI_CHECK(hipGetLastError());
-  return 0;
+  return a.K == 8192 ? launch_splitk<8192>(a, part, ln_w, ln_b, eps, xn, ldxn, s)
+                     : launch_splitk<2048>(a, part, ln_w, ln_b, eps, xn, ldxn, s);
 }
 
 extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream) {

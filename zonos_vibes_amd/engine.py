@@ -112,6 +112,9 @@ class HipEngine:
         # (256, + 4-8 MB), 966 (256, + 16 MB), 974 (512, + 8 MB) (profiles/r03_prefetch_ab.jsonl)
         self.prefetch_blocks = 256
         self.prefetch_fc1_mb = 8
+        # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
+        # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
+        self.prefetch_second = "fc1"
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
         # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
         # device: fc1's weights stream while the out_proj chain runs (identical bits). Off: it loses to the
@@ -127,9 +130,11 @@ class HipEngine:
         # hand-off of the chain takes 3-5 us under the weight stream against ~1.5 on an idle memory system,
         # DESIGN.md §5)
         self.attn_ffn = False
-        # fc2 over >= `splitk_rows` rows as a split-K GEMM (zmi_gemv_splitk: each column block reads the
-        # activation rows once; identical bits); 0 = never
+        # fc2 (K = 8192) over >= `splitk_rows` rows and out_proj (K = 2048) over >= `splitk_o_rows` rows as
+        # split-K GEMMs (zmi_gemv_splitk: each column block reads the activation rows once, and the reduce can
+        # write the next LayerNorm; identical bits); 0 = never
         self.splitk_rows = 16
+        self.splitk_o_rows = 0
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
@@ -279,9 +284,9 @@ class HipEngine:
         _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
 
     def _use_splitk(self, a, epi) -> bool:
-        return (self.splitk_rows > 0 and a.M >= self.splitk_rows and a.K == 8192 and epi == _lib.EPI_RESIDUAL
-                and not a.ln_w and a.N % 64 == 0 and a.n_valid == a.N
-                and a.M * a.N * 8 <= self.splitk_part.numel())
+        lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows}.get(a.K, 0)
+        return (lo > 0 and a.M >= lo and epi == _lib.EPI_RESIDUAL and not a.ln_w and a.pro == _lib.PRO_AUTO
+                and a.N % 64 == 0 and a.n_valid == a.N and a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
 
     def _build_plan(self):
         """Invalidate the per-row-count decode plans and graphs (new weights or buffers)."""
@@ -385,8 +390,12 @@ class HipEngine:
                     pf = _lib.Prefetch()
                     if self.prefetch_blocks > 0:
                         pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
-                        pf.ptr[1] = lw["fc1"].data_ptr()
-                        pf.bytes[1] = min(lw["fc1"].numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
+                        if self.prefetch_second == "qkv":
+                            nw = w["heads"] if i + 1 == len(w["layers"]) else w["layers"][i + 1]["qkv"]
+                        else:
+                            nw = lw["fc1"]
+                        pf.ptr[1] = nw.data_ptr()
+                        pf.bytes[1] = min(nw.numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
                         pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
                     plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form))))
                 else:
@@ -399,7 +408,12 @@ class HipEngine:
                                         ln=(lw["ln2_w"], lw["ln2_b"]))
                     plan.append(("ffnblk", (o_item[0], f_item[0], i)))
                 else:
-                    plan.append(("gemv", o_item))
+                    if pre and self._use_splitk(*o_item) and d == 2048:
+                        # the split-K reduce also writes LayerNorm(new x) for fc1 (no pre-pass launch)
+                        plan.append(("splitkln", (o_item, (lw["ln2_w"], lw["ln2_b"]))))
+                        ln_ready[0] = True
+                    else:
+                        plan.append(("gemv", o_item))
                     xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
                     plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
                                                     self.F, ln=ln)))
