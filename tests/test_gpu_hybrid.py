@@ -361,6 +361,7 @@ def test_attn_block_addln_bit_identical_to_separate():
     res = []
     for fused in (True, False):
         m.engine.attn_block = fused
+        m.engine.attn_block_rows = 16  # the fused forms at 16 rows too (the default stops at 8: speed only)
         m.engine._build_plan()
         assert any(it[0] == "attnblk" for it in m.engine._plan(2, m.engine._segments(1, 1)[0][1])) == fused
         one = m.generate(conds[0], max_new_tokens=30, sampling_params=sp, progress_bar=False)

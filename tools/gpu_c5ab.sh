@@ -1,4 +1,8 @@
-# C2 step A/B: prefetch role sizes with the separate out_proj / fc1 launches
+# C5-shaped A/B at 4 and 8 rows: fused QKV + attention forms vs separate launches
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u tools/step_ab.py '[{"prefetch_blocks": 256, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 4}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 16}, {"prefetch_blocks": 384, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 512, "prefetch_fc1_mb": 8}, {"prefetch_blocks": 512, "prefetch_fc1_mb": 16}, {"prefetch_blocks": 128, "prefetch_fc1_mb": 4}, {"prefetch_blocks": 256, "prefetch_fc1_mb": 8}]' > gpurun_out/pf_ab3.jsonl 2>gpurun_out/pf_ab3.err || exit $?
+for sl in 2 4; do
+for o in '{}' '{"attn_block_rows": 2}' '{"attn_forms": ["split"]}' '{"attn_block_rows": 4}' '{}' '{"attn_block_rows": 2}' '{"attn_forms": ["split"]}' '{"attn_block_rows": 4}'; do
+  timeout -k 10 200 python -u tools/bench_c5.py 1000 "$o" $sl >> gpurun_out/abr2_c5.jsonl 2>>gpurun_out/abr2_c5.err || exit $?
+done
+done

@@ -105,6 +105,12 @@ class HipEngine:
         # "xs" (slices exchange scores, < 1280); beyond, separate launches. The form is picked per run
         # of steps from host-side position bounds; all forms give identical bits
         self.attn_forms = ("split", "xs")
+        # the fused forms for <= `attn_block_rows` rows, "xs" for <= `attn_xs_rows`: C5-shaped steps (1000 frames
+        # after a 590-position context) at 4 / 8 / 16 rows take 1.232 / 1.516 / 1.902 ms with the fused forms,
+        # 1.267 / 1.554 / 1.730 with separate QKV + attention launches, 1.223 / 1.516 / 1.80 without "xs"
+        # (profiles/r03_attn_block_rows_ab.jsonl)
+        self.attn_block_rows = 8
+        self.attn_xs_rows = 2
         self.attn_self_slices = 8
         # prefetch-only workgroups in that launch warm the Infinity Cache with out_proj's weights and the
         # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only). With out_proj and fc1 as
@@ -313,9 +319,10 @@ class HipEngine:
         """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
         QKV and attention launches (any position)."""
         out = []
-        if self.attn_block and rows <= 16 and self.d == 2048 and self.H == 4 * self.Hkv:
+        if self.attn_block and rows <= self.attn_block_rows and self.d == 2048 and self.H == 4 * self.Hkv:
             for f in self.attn_forms:
-                out.append((f, self.lib.zmi_attn_block_max_pos(self._block_slices(f))))
+                if f != "xs" or rows <= self.attn_xs_rows:
+                    out.append((f, self.lib.zmi_attn_block_max_pos(self._block_slices(f))))
         return out + [("none", 1 << 30)]
 
     def _use_attn_block(self, rows: int, form: str | None = None) -> bool:
