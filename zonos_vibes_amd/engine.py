@@ -138,9 +138,10 @@ class HipEngine:
         self.attn_ffn = False
         # fc2 (K = 8192) over >= `splitk_rows` rows and out_proj (K = 2048) over >= `splitk_o_rows` rows as
         # split-K GEMMs (zmi_gemv_splitk: each column block reads the activation rows once, and the reduce can
-        # write the next LayerNorm; identical bits); 0 = never
+        # write the next LayerNorm; identical bits); 0 = never. out_proj split-K: C5-shaped 16-row step 1.732 vs
+        # 1.741 ms, C3 sample 151.3 vs 149.5x (profiles/r03_splitk_oproj2_ab.jsonl)
         self.splitk_rows = 16
-        self.splitk_o_rows = 0
+        self.splitk_o_rows = 16
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
