@@ -55,8 +55,13 @@ def run(pos_list, slots=1, reps=20):
         r = torch.cat(rel)
         med = [round(float(r[:, i][~r[:, i].isnan()].median()), 2) if (~r[:, i].isnan()).any() else None for i in range(8)]
         mx = [round(float(r[:, i][~r[:, i].isnan()].max()), 2) if (~r[:, i].isnan()).any() else None for i in range(8)]
-        print(json.dumps(dict(pos=p, workgroups=int(live.sum()), median_us=med, max_us=mx)), flush=True)
+
+        def q(f):
+            return [round(float(r[:, i][~r[:, i].isnan()].quantile(f)), 2) if (~r[:, i].isnan()).any() else None
+                    for i in range(8)]
+        print(json.dumps(dict(pos=p, rows=rows, workgroups=int(live.sum()), p10_us=q(0.1), median_us=med, p90_us=q(0.9),
+                              max_us=mx)), flush=True)
 
 
 if __name__ == "__main__":
-    run([int(a) for a in sys.argv[1:]] or [300, 591])
+    run([int(a) for a in sys.argv[1:]] or [300, 591], slots=int(os.environ.get("ATTN_SLOTS", "1")))

@@ -12,6 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+from zonos_vibes_amd import _lib  # noqa: E402
 from zonos_vibes_amd.config import zonos_v01_transformer  # noqa: E402
 from zonos_vibes_amd.model import Zonos  # noqa: E402
 
@@ -22,7 +23,10 @@ def main():
                         max_prefill=bench.LC + 1)
     opts = json.loads(sys.argv[1]) if len(sys.argv) > 1 else {}
     for k, v in opts.items():
-        setattr(m.engine, k, v)
+        if k.startswith("opt_"):  # library launch knobs: opt_gemm_rows -> zmi_set_option(OPT_GEMM_ROWS)
+            _lib.check(m.engine.lib.zmi_set_option(getattr(_lib, "OPT_" + k[4:].upper()), int(v)), k)
+        else:
+            setattr(m.engine, k, v)
     m.engine._build_plan()
     print(json.dumps(dict(bench.time_batch(m, dev), opts=opts)), flush=True)
 

@@ -32,6 +32,7 @@
 #include "zmi_kernels.h"
 #include "zmi_attn_merge.h"
 #include "zmi_attn_ds.h"
+#include "zmi_gemv_impl.h"
 
 namespace {
 
@@ -43,7 +44,7 @@ constexpr unsigned SPIN_LIMIT = 1u << 20;
 
 
 template <int G>
-__global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 : 1, 8))) void attn_kernel(const AttnArgs a) {
   __shared__ float sc[G][CH];
   __shared__ __attribute__((aligned(16))) bf16_t pb[G][CH];
   __shared__ float opart[NWC][G][HD];
@@ -67,9 +68,14 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
   const int c16 = lane & 15, h4 = lane >> 4;
   ZMI_ASTAMP(0);
 
-  // ---- q (A operand: row = head, zero rows past G) and this wave's K rows (B operand) ----
+  // ---- q (A operand: row = head, zero rows past G) and this wave's K rows (B operand). With G = 4 the
+  // group's q (4 heads x 128 dims = 1 KiB) comes into LDS by one LDS-DMA piece, so no q registers are live
+  // under the K / V loads (98 -> 78 VGPRs: 6 workgroups per CU instead of 4) ----
+  __shared__ __attribute__((aligned(16))) bf16_t qs[G == 4 ? G * HD : 8];
   uint4 qf[4];
-  {
+  if constexpr (G == 4) {
+    if (wave == 0) zmi_gemv::dma_piece(a.q + (size_t)qi * a.ldq + kh * G * HD + lane * 8, qs);
+  } else {
     const bool real = c16 < G;
     const bf16_t* qr = a.q + (size_t)qi * a.ldq + (kh * G + (real ? c16 : 0)) * HD + 8 * h4;
 #pragma unroll
@@ -97,12 +103,23 @@ __global__ __launch_bounds__(NT) void attn_kernel(const AttnArgs a) {
       vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
   }
 
-  // ---- scores s = fp32(q . k) * scale; keys past the position are -inf ----
+  if constexpr (G == 4) {  // the q piece (issued before the 16 K / V loads, which complete after it)
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __syncthreads();
+  }
+  // ---- scores s = fp32(q . k) * scale (dim blocks in order per key tile); keys past the position are -inf ----
+  f32x4_t st[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    uint4 qv = qf[db];
+    if constexpr (G == 4)
+      qv = c16 < G ? *reinterpret_cast<const uint4*>(&qs[c16 * HD + 8 * h4 + 32 * db]) : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) st[tt] = mfma16(qv, kf[tt][db], st[tt]);
+  }
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int db = 0; db < 4; ++db) s = mfma16(qf[db], kf[tt][db], s);
+    const f32x4_t s = st[tt];
     const int key = wave * 32 + 16 * tt + c16;  // accumulator: column = key, row = head 4 h4 + i
     if (h4 == 0) {
 #pragma unroll

@@ -635,7 +635,11 @@ template <int EPI, int GPW>
 __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const ZmiGemvArgs a, int n_cb, int n_rt,
                                                                         int rpw) {
   constexpr int W = 4, NL = 8, RT = GR_RT, K = 2048, KC = K / 64, XROW = GR_XROW, NE = 2;
-  constexpr int NGS = GR_G / GPW, NWV = NGS * W, PPW = RT * (K / 512) / NWV;  // group sets, waves, DMA pieces / wave
+  constexpr int NGS = GR_G / GPW, NWV = NGS * W;  // group sets, waves
+  // the activation tiles are DMA'd by the upper half of the waves only (PPW pieces each): the epilogue waves
+  // (wave < 8) then never wait on memory inside the tile loop, so their output stores stay in flight
+  constexpr int NDW = NWV / 2, PPW = RT * (K / 512) / NDW;
+  static_assert(NDW >= GR_G, "the epilogue waves and the DMA waves are disjoint");
   // operand pieces per tile, issued by the last wave: residual inputs (16 rows x 8 groups x 16 B), or the rows'
   // positions and cache rows (dwords)
   constexpr int EP = EPI == ZMI_EPI_RESIDUAL ? 2 : (EPI == ZMI_EPI_QKV ? 1 : 0);
@@ -663,15 +667,18 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
   const int rt_end = min(n_rt, t0 + rpw);
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X);
   const bool opw = EP && wave == NWV - 1;  // the operand-piece wave
+  const bool dw = wave >= NDW;              // a DMA wave
   if (tid == 0) *cnt = 0;
+  volatile __attribute__((address_space(3))) unsigned* lcnt = (volatile __attribute__((address_space(3))) unsigned*)cnt;
 
   // tile t = 16 rows x 4 KiB = 64 DMA pieces, PPW per wave (rows past M re-read row M - 1: their outputs are
   // discarded, and the waves' counts are fixed, which the vmcnt waits rely on), then its epilogue operands
   auto dma_tile = [&](int t) {
+    if (!dw) return;
     bf16_t* dst = xs + (t & 1) * RT * XROW;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int pc = wave + NWV * i, r = pc >> 2, p = pc & 3;
+      const int pc = wave - NDW + NDW * i, r = pc >> 2, p = pc & 3;
       const int sr = min(t * RT + r, a.M - 1);
       dma_piece(X + (size_t)sr * a.ldx + p * 512 + lane * 8, dst + r * XROW + p * 512);
     }
@@ -711,13 +718,10 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
       for (int h = 0; h < GPW; ++h) wf[h][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc[h], lane * 16, j * 1024, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
-  // the first tile's pieces: issued before the second tile's and the weights
-  if (t0 + 1 >= rt_end)
-    ZMI_WAIT_VM(GPW * NL);
-  else if (opw)
-    ZMI_WAIT_VM(GPW * NL + PPW + EP);
-  else
-    ZMI_WAIT_VM(GPW * NL + PPW);
+  // every weight slice and the first two tiles' pieces: waiting here for all of them keeps the compiler's own
+  // waits for the weights out of the tile loop (a vmcnt(0) there would also wait for the DMA of later tiles
+  // and for the epilogue stores)
+  ZMI_WAIT_VM(0);
   __syncthreads();
 
   for (int t = t0;; ++t) {  // invariant: tile t's rows and operands are in LDS, visible to every wave
@@ -747,7 +751,7 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
     // the previous tile's epilogues have read the segment sums (bounded: they are a few hundred cycles of work)
     if (ti > 0) {
       const unsigned want = (unsigned)(n_ew * ti);
-      for (int spin = 0; *reinterpret_cast<volatile unsigned*>(cnt) < want && spin < (1 << 20); ++spin)
+      for (int spin = 0; *lcnt < want && spin < (1 << 20); ++spin)
         __builtin_amdgcn_s_sleep(1);
     }
     {
@@ -777,8 +781,12 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
         q_kvr = reinterpret_cast<const int*>(od)[16 + (lane >> 2)];
       }
     }
-    ZMI_WAIT_VM(0);  // the next tile's pieces
-    __syncthreads();  // segment sums complete; the next tile's rows visible; this tile's buffers free
+    if (dw) ZMI_WAIT_VM(0);  // the next tile's pieces (DMA waves; the epilogue waves' stores stay in flight)
+    // segment sums complete; the next tile's rows visible; this tile's buffers free (LDS-only fence: no wait
+    // for global stores)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (ti == 1) ZMI_GSTAMP(4);
     if (t + 2 < rt_end) dma_tile(t + 2);
     if (ew) {
