@@ -87,7 +87,7 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
     return tot / (reps * len(items))
 
 
-PMC_FILE = "r03_pmc_fc1_fetch.json"
+PMC_FILE = "r03c_pmc_fc1_fetch.json"
 
 
 def pmc_traffic():
@@ -744,7 +744,7 @@ def main():
                                     "unit": "TFLOP/s", "frac": round(dac_tf / MFMA_PEAK_TFLOPS, 4),
                                     "flop_per_frame": DAC_FLOP_PER_FRAME, "frames": n_new,
                                     "ms": breakdown["dac_decode_ms"],
-                                    "mfma_busy_source": "profiles/r03_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
+                                    "mfma_busy_source": "profiles/r03c_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
             "c3_sharded": c3,
             "widened": widened,
             "end_of_batch_gather": gather,

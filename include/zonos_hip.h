@@ -70,9 +70,9 @@ typedef struct ZmiGemvArgs {
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
 /* One kernel for every M: a row's result is bit-identical whatever the batch it is computed in. */
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
-/* Many-row fc2 (K = 8192, EPI_RESIDUAL, plain): a split-K GEMM (one workgroup per 64-column block and 1024-element
- * K segment, fp32 segment sums in `part`, then a reduce launch adding the segments in K order + the residual
- * epilogue). Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment MFMA chains and segment
+/* Many-row fc2 (K = 8192) or out_proj (K = 2048), EPI_RESIDUAL, plain (reference _torch.py:100-101,141,152): a
+ * split-K GEMM (one workgroup per 64-column block and K segment -- 8 x 1024 / 4 x 512, the GEMV's wave split --,
+ * fp32 segment sums in `part`, then a reduce launch adding the segments in K order + the residual epilogue). Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment MFMA chains and segment
  * order); reads the activation rows once per column block instead of once per column group. part:
  * zmi_gemv_splitk_floats(M, N) floats. */
 int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream);
