@@ -96,8 +96,8 @@ class HipEngine:
         self.sptr = self.stream.cuda_stream
         self.w = None
         self.attn_variant = 0  # zmi_attention_variant kernel choice (0 = library; all give identical bits)
-        # decode QKV + attention as ONE launch (zmi_attn_block) where it applies: <= 16 rows and
-        # positions below the whole-query kernel's reach; identical bits either way (speed only)
+        # decode QKV + attention as ONE launch (zmi_attn_block) where it applies: <= `attn_block_rows` rows
+        # and positions below the fused forms' reach; identical bits either way (speed only)
         self.attn_block = True
         self.attn_block_slices = 8
         # fused forms tried in order, each where every row's position is below its reach: "split" (one
