@@ -15,6 +15,7 @@ value = total audio seconds over all ranks / max-over-ranks wall time of the K t
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -185,13 +186,25 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
                 us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
                 hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk),
                 note="QKV weights + the layer's K/V of both rows; the launch also prefetches out_proj's weights")
+        # the sampler launches captured in one graph: a Python-side launch costs more than the kernel, so
+        # back-to-back launches from the host would time the host
+        n_s = 8 * reps
+        _lib.check(e.lib.zmi_graph_begin(e.sptr), "graph_begin")
+        try:
+            for _ in range(n_s):
+                e._sample(e.logits, None, 0, 0, 1)
+        finally:
+            g = ctypes.c_void_p()
+            _lib.check(e.lib.zmi_graph_end(e.sptr, ctypes.byref(g)), "graph_end")
+        _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")  # warm
         st.record(e.stream)
-        for _ in range(reps):
-            e._sample(e.logits, None, 0, 0, 1)
+        _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")
         en.record(e.stream)
         en.synchronize()
-        out["sampler (CFG + penalty + argmax + FSM + next embedding)"] = dict(
-            us=round(st.elapsed_time(en) * 1000.0 / reps, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
+        _lib.check(e.lib.zmi_graph_destroy(g.value))
+        kind = "greedy: one workgroup per slot" if e._greedy_step(0, 1) else "per-codebook workgroups"
+        out[f"sampler (CFG + penalty + argmax + FSM + next embedding; {kind})"] = dict(
+            us=round(st.elapsed_time(en) * 1000.0 / n_s, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
     e.check_errors()
     e.release(0)
     return {"pos": pos, "kernels": out}
