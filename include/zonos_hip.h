@@ -169,6 +169,35 @@ int zmi_attn_ffn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* out_proj, cons
                        void* ogran, void* rgran, unsigned* err, void* attn_out, int ldo, void* stream);
 int64_t zmi_attn_ffn_gran_words(int rows);
 int zmi_attn_ffn_max_pos(void);
+/* Persistent decode launch of a block's second half at batch 1 (reference _torch.py:100-101 out_proj +
+ * residual, :101 norm2, :147-152 fc1 + SwiGLU + fc2, and the second residual add): 256 workgroups, one per CU
+ * (needs 256 CUs), each streaming its slice of out_proj, fc1 and fc2 through an LDS ring (non-temporal
+ * LDS-DMA) that runs ahead of the in-launch hand-offs ({value, tag = position + 1} granules in `gran`:
+ * zmi_ffn_engine_gran_words(M) u64 words per layer; zero a row's words when it starts a new utterance).
+ * x (bf16 [M][ldx]) is updated in place to x + out_proj(attn) + fc2(SwiGLU(fc1(norm2(.)))) bit-identically to
+ * zmi_gemv_launch(out_proj, EPI_RESIDUAL), zmi_gemv_launch(fc1 with the norm2 LayerNorm, EPI_SWIGLU) and
+ * zmi_gemv_launch(fc2, EPI_RESIDUAL); h (optional) receives the SwiGLU rows. d_model 2048, d_ff 8192 (packed
+ * weights as zmi_pack_weight), 1 <= M <= 2. *err becomes nonzero if a wait gave up. diag: NULL, or u64
+ * [256][16] phase stamps (s_memrealtime, diagnostics). */
+typedef struct ZmiFfnEngineArgs {
+  const void* w_out;    /* packed out_proj [2048][2048]                                       */
+  const void* w_fc1;    /* packed fc1 [16384][2048] (ZMI_PACK_SWIGLU)                           */
+  const void* w_fc2;    /* packed fc2 [2048][8192]                                              */
+  const void* ln_w;     /* norm2 weight / bias, bf16 [2048]                                     */
+  const void* ln_b;
+  float eps;
+  int M;
+  const void* attn;     /* bf16 [M][ld_attn] attention output rows                              */
+  void* x;              /* bf16 [M][ldx] residual rows, updated in place                        */
+  void* h;              /* bf16 [M][ldh] SwiGLU rows, or NULL                                   */
+  int ld_attn, ldx, ldh, reserved;
+  const int* row_pos;   /* [M] positions (tags = position + 1)                                  */
+  void* gran;
+  unsigned* err;
+  void* diag;
+} ZmiFfnEngineArgs;
+int zmi_ffn_engine(const ZmiFfnEngineArgs* args, void* stream);
+int64_t zmi_ffn_engine_gran_words(int rows);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);
@@ -364,8 +393,12 @@ int zmi_version(void);
  *   32-column tile loop; 0 = always the tile loop.
  *   ZMI_OPT_AF_DEPTH (default 3): weight loads each streaming wave of zmi_attn_ffn_block keeps in flight (1 KiB
  *          each; 2, 3, 4, 6 or 0 = unthrottled): the launch's latency-bound hand-offs queue behind whatever the
- *          chip has in flight, so the weight stream is issued progressively. */
-enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_COUNT = 4 };
+ *          chip has in flight, so the weight stream is issued progressively.
+ *   ZMI_OPT_ENG_START (default 1): how zmi_ffn_engine's ring starts: 0 = every slot at once, 1 = the out_proj slot
+ *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
+ *   ZMI_OPT_ENG_SPARE: reserved for engine experiments (0). */
+enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
+       ZMI_OPT_ENG_SPARE = 5, ZMI_OPT_COUNT = 6 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

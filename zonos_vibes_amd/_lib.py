@@ -21,6 +21,8 @@ OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
 OPT_GEMM_ROWS = 1
 OPT_AF_DEPTH = 2
 OPT_AF_DELAY = 3
+OPT_ENG_START = 4
+OPT_ENG_SPARE = 5
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
@@ -44,6 +46,15 @@ class GemvArgs(ctypes.Structure):
 class Prefetch(ctypes.Structure):
     _fields_ = [("ptr", c_void_p * 2), ("bytes", c_int64 * 2), ("sink", c_void_p), ("blocks", c_int),
                 ("reserved", c_int)]
+
+
+class FfnEngineArgs(ctypes.Structure):
+    _fields_ = [
+        ("w_out", c_void_p), ("w_fc1", c_void_p), ("w_fc2", c_void_p), ("ln_w", c_void_p), ("ln_b", c_void_p),
+        ("eps", c_float), ("M", c_int), ("attn", c_void_p), ("x", c_void_p), ("h", c_void_p),
+        ("ld_attn", c_int), ("ldx", c_int), ("ldh", c_int), ("reserved", c_int),
+        ("row_pos", c_void_p), ("gran", c_void_p), ("err", c_void_p), ("diag", c_void_p),
+    ]
 
 
 class Sampling(ctypes.Structure):
@@ -101,6 +112,8 @@ _SIGS = {
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
     "zmi_ffn_block_gran_words": (c_int64, [c_int]),
+    "zmi_ffn_engine": (c_int, [ctypes.POINTER(FfnEngineArgs), c_void_p]),
+    "zmi_ffn_engine_gran_words": (c_int64, [c_int]),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,
