@@ -198,6 +198,46 @@ typedef struct ZmiFfnEngineArgs {
 } ZmiFfnEngineArgs;
 int zmi_ffn_engine(const ZmiFfnEngineArgs* args, void* stream);
 int64_t zmi_ffn_engine_gran_words(int rows);
+/* Persistent decode launch of one whole transformer block at batch 1 (reference _torch.py:136 attention, :140
+ * out_proj + residual :100-101, norm2, :147-152 fc1 + SwiGLU + fc2 + residual), then the NEXT op on the new
+ * residual rows: next = 0: LayerNorm (lnn) + QKV projection of layer L + 1 (:114-126: RoPE, K / V of the rows'
+ * positions into k_next / v_next, q overwritten with the next layer's q); next = 1 (last layer): norm_f (lnn) +
+ * the 9 heads (model.py:100-101) into logits f32 [M][9][1026]. The attention reads q and this layer's caches as the
+ * previous launch (the QKV GEMV of layer 0, or the previous layer's engine) left them. 256 workgroups, one per CU
+ * (needs 256 CUs), streaming every weight of the layer through per-wave LDS-DMA rings that run ahead of the
+ * in-launch hand-offs ({value, tag = position + 1} granules in `gran`: zmi_layer_engine_gran_words(M) u64 words
+ * per layer; zero them when the rows start a new utterance). Positions <= zmi_layer_engine_max_pos(). Every output
+ * is bit-identical to zmi_attention + the zmi_gemv_launch plan (out_proj RESIDUAL, fc1 LayerNorm SWIGLU, fc2
+ * RESIDUAL, next QKV / LOGITS with the LayerNorm prologue). attn_out (optional) receives the attention rows.
+ * d_model 2048, d_ff 8192, 16 query / 4 kv heads of 128, 1 <= M <= 2 (row r caches into KV row r). */
+typedef struct ZmiLayerEngineArgs {
+  const void* w_out;    /* packed out_proj [2048][2048]                                         */
+  const void* w_fc1;    /* packed fc1 [16384][2048] (ZMI_PACK_SWIGLU)                             */
+  const void* w_fc2;    /* packed fc2 [2048][8192]                                                */
+  const void* w_next;   /* packed QKV [3072][2048] of layer L + 1, or the heads [9248][2048]      */
+  const void* ln2_w;    /* norm2, bf16 [2048]                                                     */
+  const void* ln2_b;
+  const void* lnn_w;    /* norm of layer L + 1, or norm_f                                         */
+  const void* lnn_b;
+  float eps;
+  int M, smax, next;
+  const int* row_pos;   /* [M] positions (tags = position + 1)                                    */
+  void* x;              /* bf16 [M][2048] residual rows, updated in place                         */
+  void* q;              /* bf16 [M][2048] this layer's q; the next layer's q on return (QKV)      */
+  const void* k_cache;  /* this layer's K [M][4][smax][128] and V^T [M][4][128][smax]             */
+  const void* v_cache;
+  void* k_next;         /* the next layer's caches (next = 0)                                     */
+  void* v_next;
+  const float* rope;    /* (cos, sin) table as for zmi_gemv_launch (next = 0)                     */
+  void* attn_out;       /* optional bf16 [M][2048]                                                */
+  float* logits;        /* next = 1                                                               */
+  void* gran;
+  unsigned* err;
+  void* diag;           /* NULL, or u64 [256][32] phase stamps (diagnostics)                      */
+} ZmiLayerEngineArgs;
+int zmi_layer_engine(const ZmiLayerEngineArgs* args, void* stream);
+int64_t zmi_layer_engine_gran_words(int rows);
+int zmi_layer_engine_max_pos(void);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);

@@ -443,6 +443,22 @@ def test_sampler_noise_is_exponential():
     assert len(set(out.flatten().tolist())) > 350
 
 
+def test_sample_from_logits_v1025_mask_tokens_penalise_eos():
+    """Unpadded heads (V = 1025): the reference clamps the penalty window to V - 1 = 1024 (sampling.py:111), so a
+    mask token (1025) in the window penalises the EOS column. Greedy, against oracle.zonos_cpu's restatement."""
+    from zonos_vibes_amd.sampling import sample_from_logits
+    g = torch.Generator().manual_seed(5)
+    logits = torch.randn(4, 9, 1025, generator=g)
+    logits[..., 1024] = logits.max(dim=-1).values + 0.5  # EOS wins unless it is penalised
+    gen = torch.randint(0, 1024, (4, 9, 3), generator=g)
+    gen[:2, :, -1] = 1025  # mask tokens in the window of batch rows 0, 1
+    ref = oz.repetition_penalty(logits, gen, 3.0, 2).argmax(dim=-1)
+    out = sample_from_logits(logits.to(DEV), temperature=0.0, generated_tokens=gen.to(DEV), repetition_penalty=3.0,
+                             repetition_penalty_window=2)
+    assert torch.equal(out.squeeze(-1).cpu(), ref)
+    assert (ref[:2] != 1024).any() and (ref[2:] == 1024).all()
+
+
 def test_delay_pattern_init_and_revert():
     L = _lib()
     t, _ = load_golden("delay_pattern")

@@ -57,6 +57,17 @@ class FfnEngineArgs(ctypes.Structure):
     ]
 
 
+class LayerEngineArgs(ctypes.Structure):
+    _fields_ = [
+        ("w_out", c_void_p), ("w_fc1", c_void_p), ("w_fc2", c_void_p), ("w_next", c_void_p),
+        ("ln2_w", c_void_p), ("ln2_b", c_void_p), ("lnn_w", c_void_p), ("lnn_b", c_void_p),
+        ("eps", c_float), ("M", c_int), ("smax", c_int), ("next", c_int),
+        ("row_pos", c_void_p), ("x", c_void_p), ("q", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
+        ("k_next", c_void_p), ("v_next", c_void_p), ("rope", c_void_p), ("attn_out", c_void_p), ("logits", c_void_p),
+        ("gran", c_void_p), ("err", c_void_p), ("diag", c_void_p),
+    ]
+
+
 class Sampling(ctypes.Structure):
     _fields_ = [
         ("temperature", c_float), ("top_p", c_float), ("min_p", c_float), ("linear", c_float),
@@ -114,6 +125,9 @@ _SIGS = {
     "zmi_ffn_block_gran_words": (c_int64, [c_int]),
     "zmi_ffn_engine": (c_int, [ctypes.POINTER(FfnEngineArgs), c_void_p]),
     "zmi_ffn_engine_gran_words": (c_int64, [c_int]),
+    "zmi_layer_engine": (c_int, [ctypes.POINTER(LayerEngineArgs), c_void_p]),
+    "zmi_layer_engine_gran_words": (c_int64, [c_int]),
+    "zmi_layer_engine_max_pos": (c_int, []),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,

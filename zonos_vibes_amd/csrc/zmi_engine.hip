@@ -31,20 +31,20 @@
 #include "zmi_common.h"
 #include "zmi_kernels.h"
 #include "zmi_gemv_impl.h"
+#include "zmi_engine.h"
 
 namespace {
 
-using zmi_gemv::ror8;
+using namespace zmi_eng;
 
 constexpr int DM = 2048, FF = 8192;
 constexpr int NBLK = 256;
 constexpr int NCW = 4, NSW = 2, NWV = NCW + NSW, NT = NWV * 64;
 constexpr int MAXR = 2;
-constexpr int SLOT = 8192, DEPTH = 4;
+constexpr int DEPTH = 4;
 constexpr int NSLOT = 13;                 // out_proj 1 + fc1 8 + fc2 2 x 2 slots per consumer wave
 constexpr int XROW = DM + 8;
 constexpr int GX_W = DM / 2, GH_W = FF / 2, GP_W = 256 * 8 * 8;  // granule words per row
-constexpr unsigned SPIN = 1u << 20;
 
 // LDS
 constexpr size_t L_RING = 0;                                            // [NCW][DEPTH][8 KiB]
@@ -57,8 +57,6 @@ constexpr size_t L_BYTES = L_CNT + 16 * 4;
 static_assert(L_BYTES <= 160 * 1024, "LDS");
 static_assert(L_BUFA % 16 == 0 && L_BUFB % 16 == 0 && L_CNT % 16 == 0, "alignment");
 enum { C_READY = 0, C_O = 1, C_F1 = 2 };  // C_F1 + j: fc1 group j
-
-typedef __attribute__((address_space(3))) unsigned lds_u32;
 
 struct Args {
   const char* w_out;
@@ -79,43 +77,9 @@ struct Args {
   int start, spare;  // ZMI_OPT_ENG_START / _SPARE
 };
 
-__device__ __forceinline__ void give_up(unsigned* err) {
-  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ void stamp(const Args& a, int i) {
   if (a.diag && (threadIdx.x & 63) == 0)
     a.diag[(size_t)blockIdx.x * 16 + i] = __builtin_amdgcn_s_memrealtime();
-}
-
-__device__ __forceinline__ lds_u32* lds_cnt(char* smem, int i) {
-  return reinterpret_cast<lds_u32*>((__attribute__((address_space(3))) char*)smem + L_CNT + 4 * i);
-}
-
-// LDS arrival: this wave's LDS writes, then one lane's add
-__device__ __forceinline__ void lds_arrive(lds_u32* c, int lane) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_wait_ge(lds_u32* c, unsigned want, unsigned* err) {
-  for (unsigned spin = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want; ++spin) {
-    if (spin > SPIN) {
-      give_up(err);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// one 1 KiB LDS-DMA piece, non-temporal (lane-linear: lane l's 16 B land at lds + 16 l). Inline asm: the
-// compiler does not count it; the consumer's own vmcnt waits do (cdna_hip_programming.md §5.7)
-__device__ __forceinline__ void dma_nt(const char* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
 }
 
 // slot k of consumer wave c in block b: 8 KiB of one weight matrix (M8 layout: group g's chunks
@@ -131,26 +95,7 @@ __device__ __forceinline__ const char* slot_src(const Args& a, int k, int b, int
   return a.w_fc2 + ((size_t)g * 128 + s * 16 + (kk & 1) * 8) * 1024;
 }
 
-__device__ __forceinline__ void issue_slot(const char* src, unsigned lds, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot have returned
-  const char* g = src + lane * 16;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dma_nt(g + j * 1024, lds + j * 1024);
-}
-
-// slot landed: `after` slots (8 DMA pieces each) were issued after it; loads complete in order, so the
-// stores a wave issues in between only make the wait longer
-__device__ __forceinline__ void wait_slot(int after) {
-  if (after <= 0)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (after == 1)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (after == 2)
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-}
-static_assert(DEPTH == 4, "wait_slot covers up to 3 slots issued after the awaited one");
+__device__ __forceinline__ lds_u32* lds_cnt(char* smem, int i) { return lds_word(smem, L_CNT + 4 * i); }
 
 __device__ __forceinline__ void consumer(const Args& a, char* smem, int b, int c, int lane, const unsigned (&tag)[MAXR]) {
   const unsigned ring = __builtin_amdgcn_readfirstlane(
@@ -246,61 +191,6 @@ __device__ __forceinline__ void consumer(const Args& a, char* smem, int b, int c
       if (k == NSLOT - 1 && c == 0) stamp(a, 10);
     }
   }
-}
-
-// one wave gathers n = 64 PER granules g[0 .. n) carrying `tag` into dst[0 .. n) (their low words)
-template <int PER>
-__device__ __forceinline__ void gather(const uint64_t* g, uint32_t* dst, uint32_t tag, int lane, unsigned* err) {
-  uint32_t pend = PER >= 32 ? 0xffffffffu : ((1u << PER) - 1u);
-  for (unsigned spin = 0;; ++spin) {
-    uint64_t v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = ((pend >> i) & 1) ? ld_wt64(g + lane + 64 * i) : 0ull;
-#pragma unroll
-    for (int i = 0; i < PER; ++i)
-      if (((pend >> i) & 1) && (uint32_t)(v[i] >> 32) == tag) {
-        dst[lane + 64 * i] = (uint32_t)v[i];
-        pend &= ~(1u << i);
-      }
-    if (__all(pend == 0)) break;
-    if (spin > SPIN) {
-      give_up(err);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// nn.LayerNorm of one 2048-element bf16 row in LDS, in place, by one wave: the GEMV LayerNorm prologue's
-// arithmetic (zmi_common.h: 4 parts of 512, lane L's chunk 8 L of each part, part sums by wave_sum,
-// (p0 + p1) + (p2 + p3), two passes)
-__device__ __forceinline__ void ln_row(bf16_t* xr, const bf16_t* gw, const bf16_t* gb, float eps, int lane) {
-  constexpr int NQ = 4;
-  uint4 xv[NQ], gv[NQ], bv[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    gv[q] = *reinterpret_cast<const uint4*>(gw + q * 512 + lane * 8);
-    bv[q] = *reinterpret_cast<const uint4*>(gb + q * 512 + lane * 8);
-    xv[q] = *reinterpret_cast<const uint4*>(xr + q * 512 + lane * 8);
-  }
-  float part[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    float t = 0.f;
-    t += ln_chunk_sum(xv[q], 0.f, false);
-    part[q] = wave_sum(t);
-  }
-  const float mean = ln_combine<NQ>(part) / (float)DM;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    float t = 0.f;
-    t += ln_chunk_sum(xv[q], mean, true);
-    part[q] = wave_sum(t);
-  }
-  const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part) / (float)DM + eps), nbias = -mean * rstd;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-    *reinterpret_cast<uint4*>(xr + q * 512 + lane * 8) = ln_apply(xv[q], gv[q], bv[q], rstd, nbias);
 }
 
 __device__ __forceinline__ void service(const Args& a, char* smem, int b, int r, int lane, const unsigned (&tag)[MAXR]) {

@@ -140,6 +140,13 @@ class HipEngine:
         # split-K GEMMs (zmi_gemv_splitk: each column block reads the activation rows once, and the reduce can
         # write the next LayerNorm; identical bits); 0 = never. out_proj split-K: C5-shaped 16-row step 1.732 vs
         # 1.741 ms, C3 sample 151.3 vs 149.5x (profiles/r03_splitk_oproj2_ab.jsonl)
+        # out_proj + norm2 + fc1 + fc2 as ONE persistent launch (zmi_ffn_engine: 256 workgroups, one per CU, LDS-DMA
+        # weight rings running ahead of the in-launch hand-offs) for <= 2 rows at the v0.1 dims; identical bits
+        self.ffn_engine = True
+        # the whole decode layer as ONE persistent launch (zmi_layer_engine: attention, out_proj, fc1, fc2 and the
+        # next layer's QKV / the heads, 256 workgroups, LDS-DMA weight rings) for <= 2 rows at the v0.1 dims and
+        # positions <= zmi_layer_engine_max_pos(); identical bits (the "engine" form)
+        self.layer_engine = True
         self.splitk_rows = 16
         self.splitk_o_rows = 16
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
@@ -183,7 +190,14 @@ class HipEngine:
             # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer; a row's
             # areas are zeroed when it starts an utterance (prefill), and its error word
             self.blk_gran = z(self.n_kv, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
-            self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block
+            self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block,
+            # [4] attn_ffn_block, [5] ffn_engine, [6] layer_engine
+            # zmi_ffn_engine hand-off granules (batch 1: rows 0 and 1), one area per layer
+            ew = self.lib.zmi_ffn_engine_gran_words(2)
+            self.eng_gran = z(self.L if S == 1 and not self.hybrid else 0, max(ew, 0), dt=torch.int64)
+            # zmi_layer_engine hand-off granules (batch 1), one area per layer
+            lw_ = self.lib.zmi_layer_engine_gran_words(2)
+            self.lay_gran = z(self.L if S == 1 and not self.hybrid else 0, max(lw_, 0), dt=torch.int64)
             # zmi_ffn_block hand-off granules (the new residual rows), one area per layer
             self.ffn_gran = z(self.L, R, self.lib.zmi_ffn_block_gran_words(1), dt=torch.int64)
             # zmi_attn_ffn_block hand-off granules (the attention output rows), one area per layer
@@ -312,6 +326,47 @@ class HipEngine:
         return (self.ffn_block and rows <= self.ffn_block_rows and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
                 and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
 
+    def _use_ffn_engine(self, rows: int) -> bool:
+        return (self.ffn_engine and rows <= 2 and self.S == 1 and self.d == 2048 and self.F == 8192
+                and self.H * self.hd == 2048 and not self.hybrid
+                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
+
+    def _use_layer_engine(self, rows: int) -> bool:
+        return (self.layer_engine and rows <= 2 and self.S == 1 and self.d == 2048 and self.F == 8192
+                and self.H == 16 and self.Hkv == 4 and self.hd == 128 and not self.hybrid
+                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
+
+    def _layer_engine_args(self, i: int, rows: int) -> _lib.LayerEngineArgs:
+        w, L = self.w, self.L
+        lw, last = w["layers"][i], i + 1 == L
+        e = _lib.LayerEngineArgs()
+        e.w_out, e.w_fc1, e.w_fc2 = lw["out"].data_ptr(), lw["fc1"].data_ptr(), lw["fc2"].data_ptr()
+        e.ln2_w, e.ln2_b = lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr()
+        if last:
+            e.w_next, e.lnn_w, e.lnn_b, e.next = w["heads"].data_ptr(), w["nf_w"].data_ptr(), w["nf_b"].data_ptr(), 1
+            e.logits = self.logits.data_ptr()
+        else:
+            nw = w["layers"][i + 1]
+            e.w_next, e.lnn_w, e.lnn_b, e.next = nw["qkv"].data_ptr(), nw["ln1_w"].data_ptr(), nw["ln1_b"].data_ptr(), 0
+            e.k_next, e.v_next, e.rope = self.kc[i + 1].data_ptr(), self.vc[i + 1].data_ptr(), self.rope.data_ptr()
+        e.eps, e.M, e.smax = self.eps, rows, self.smax
+        e.row_pos, e.x, e.q = self.row_pos.data_ptr(), self.x.data_ptr(), self.q.data_ptr()
+        e.k_cache, e.v_cache = self.kc[i].data_ptr(), self.vc[i].data_ptr()
+        e.attn_out = None
+        e.gran, e.err = self.lay_gran[i].data_ptr(), self.blk_err[6:].data_ptr()
+        return e
+
+    def _ffn_engine_args(self, lw, i: int, rows: int) -> _lib.FfnEngineArgs:
+        e = _lib.FfnEngineArgs()
+        e.w_out, e.w_fc1, e.w_fc2 = lw["out"].data_ptr(), lw["fc1"].data_ptr(), lw["fc2"].data_ptr()
+        e.ln_w, e.ln_b, e.eps = lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), self.eps
+        e.M = rows
+        e.attn, e.ld_attn = self.attn.data_ptr(), self.H * self.hd
+        e.x, e.ldx = self.x.data_ptr(), self.d
+        e.h, e.ldh = None, 0
+        e.row_pos, e.gran, e.err = self.row_pos.data_ptr(), self.eng_gran[i].data_ptr(), self.blk_err[5:].data_ptr()
+        return e
+
     def _use_attn_ffn(self, rows: int, form: str) -> bool:
         return (self.attn_ffn and form == "split" and rows * self.Hkv <= 8 and rows <= 4 and self._use_ffn_block(rows)
                 and self.H == 4 * self.Hkv and self.hd == 128)
@@ -320,6 +375,8 @@ class HipEngine:
         """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
         QKV and attention launches (any position)."""
         out = []
+        if self._use_layer_engine(rows):
+            out.append(("engine", self.lib.zmi_layer_engine_max_pos()))
         if self.attn_block and rows <= self.attn_block_rows and self.d == 2048 and self.H == 4 * self.Hkv:
             for f in self.attn_forms:
                 if f != "xs" or rows <= self.attn_xs_rows:
@@ -352,6 +409,16 @@ class HipEngine:
         """Decode-step launches for the first `rows` rows (slots 0 .. rows/2 - 1). Every kernel's
         per-row arithmetic is independent of `rows` and of the launch form, so a slot decodes
         identically in any plan."""
+        if (rows, form) not in self._plans and form == "engine":
+            # layer 0's QKV (LayerNorm prologue, RoPE, KV write), then one persistent launch per layer, the last
+            # of which also runs norm_f + the heads
+            lw0, d, qd = self.w["layers"][0], self.d, self.H * self.hd
+            qkv_n = (self.H + 2 * self.Hkv) * self.hd
+            plan = [("gemv", self._gemv(lw0["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
+                                        ln=(lw0["ln1_w"], lw0["ln1_b"]), kv=(self.kc[0], self.vc[0]),
+                                        row_kv=self.row_kv, row_pos=self.row_pos))]
+            plan += [("layereng", self._layer_engine_args(i, rows)) for i in range(self.L)]
+            self._plans[(rows, form)] = plan
         if (rows, form) not in self._plans:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
@@ -409,6 +476,9 @@ class HipEngine:
                 else:
                     plan.append(("gemv", qkv))
                     plan.append(("attn", i))
+                if self._use_ffn_engine(rows):
+                    plan.append(("ffneng", self._ffn_engine_args(lw, i, rows)))
+                    continue
                 o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
                 if self._use_ffn_block(rows):
                     o_item[0].row_pos = self.row_pos.data_ptr()
@@ -471,11 +541,12 @@ class HipEngine:
         """Raise if a launch gave up waiting on an in-launch hand-off (bounded spin) or refused a row past
         its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
         attn = int(self.attn_work[:4].view(torch.int32).item())
-        blk, mamba, _, ffn, af = (int(v) for v in self.blk_err[:5].tolist())
-        if attn or blk or mamba or ffn or af:
-            self.attn_work[:4].zero_()
-            self.blk_err[:2].zero_()
-            self.blk_err[3:5].zero_()
+        blk, mamba, _, ffn, af, eng, leng = (int(v) for v in self.blk_err[:7].tolist())
+        if attn or blk or mamba or ffn or af or eng or leng:
+            with torch.cuda.stream(self.stream):  # ordered with the engine's launches
+                self.attn_work[:4].zero_()
+                self.blk_err[:2].zero_()
+                self.blk_err[3:7].zero_()
             self.stream.synchronize()
         if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
@@ -488,6 +559,11 @@ class HipEngine:
             raise RuntimeError("ffn_block: a wait for the new residual rows timed out (results are invalid)")
         if af:
             raise RuntimeError("attn_ffn_block: a hand-off wait timed out or a row was past the form's reach "
+                               "(results are invalid)")
+        if eng:
+            raise RuntimeError("ffn_engine: an in-launch hand-off wait timed out (results are invalid)")
+        if leng:
+            raise RuntimeError("layer_engine: an in-launch hand-off wait timed out or a position was past its reach "
                                "(results are invalid)")
 
     def refresh_inputs(self):
@@ -538,6 +614,10 @@ class HipEngine:
                 self._run_ffn_block(item)
             elif kind == "attnffn":
                 self._run_attn_ffn(item)
+            elif kind == "layereng":
+                _lib.check(self.lib.zmi_layer_engine(ctypes.byref(item), self.sptr), "layer_engine")
+            elif kind == "ffneng":
+                _lib.check(self.lib.zmi_ffn_engine(ctypes.byref(item), self.sptr), "ffn_engine")
             elif kind == "splitkln":
                 (a, epi), ln = item
                 _lib.check(self.lib.zmi_gemv_splitk_ln(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
@@ -635,6 +715,9 @@ class HipEngine:
         self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
         self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
         self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
+        if slot == 0:
+            self.eng_gran.zero_()
+            self.lay_gran.zero_()
 
     def _prefill_logits(self, s_len: int):
         """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""

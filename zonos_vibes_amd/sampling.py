@@ -44,7 +44,10 @@ def sample_from_logits(logits: torch.Tensor, temperature: float = 1.0, top_p: fl
     lg = logits.to(torch.float32).contiguous()
     gen, gl = None, 0
     if generated_tokens is not None and generated_tokens.shape[-1] > 0:
-        gen = generated_tokens.to(dev, torch.int32).contiguous()
+        gen = generated_tokens.to(dev, torch.int32)
+        if v == 1025:  # the reference clamps to logits.shape[-1] - 1 (sampling.py:111): the mask token 1025
+            gen = gen.clamp_max(1024)  # penalises EOS (1024), not the padding column this wrapper adds
+        gen = gen.contiguous()
         gl = gen.shape[-1]
     nz = None if noise is None else noise.to(dev, torch.float32).contiguous()
     out = torch.empty(b, 9, dtype=torch.int32, device=dev)
