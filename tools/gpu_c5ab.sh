@@ -1,6 +1,7 @@
-# C3 sample A/B: out_proj split-K upper row bound (64 vs none)
+# batched prefill (prefill_many): engine tests, C3 sample A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for o in '{"splitk_o_max_rows": 64}' '{"splitk_o_max_rows": 100000}' '{"splitk_o_max_rows": 64}' '{"splitk_o_max_rows": 100000}'; do
-  timeout -k 10 300 python -u tools/bench_batch.py "$o" >> gpurun_out/skmax_c3.jsonl 2>>gpurun_out/skmax_c3.err || exit $?
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_scale.py tests/test_gpu_generate.py tests/test_gpu_hybrid.py tests/test_gpu_c1.py tests/test_gpu_api.py > gpurun_out/pm_tests.log 2>&1 || exit $?
+for o in '{"prefill_batch": false}' '{}' '{"prefill_batch": false}' '{}'; do
+  timeout -k 10 300 python -u tools/bench_batch.py "$o" >> gpurun_out/pm_c3.jsonl 2>>gpurun_out/pm_c3.err || exit $?
 done

@@ -26,6 +26,7 @@ from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN, ZonosCon
 
 HEADS_N = N_CODEBOOKS * 1026            # 9 heads x (1025 + 1 pad row), model.py:37 + utils.py:12-27
 HEADS_N_PAD = (HEADS_N + 15) // 16 * 16
+PREFILL_BATCH_ROWS = 2048  # rows of one batched prefill pass (prefill_many): 6 C2-sized utterances (2 x 161)
 
 
 def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
@@ -72,6 +73,7 @@ def _round8(n: int) -> int:
 
 class HipEngine:
     hybrid = False
+    prefill_batch = True  # prefill_many packs several slots into one pass (the hybrid's scan does not)
 
     def __init__(self, cfg: ZonosConfig, device="cuda", max_slots: int = 1, max_seqlen: int = 2048,
                  max_prefill: int = 512):
@@ -91,6 +93,9 @@ class HipEngine:
         self.smax = min(_round8(int(max_seqlen)), ROPE_TABLE_LEN)
         self.tcap = self.smax  # delayed frames per slot never exceed KV positions
         self.max_prefill = int(max_prefill)
+        # prefill rows one pass can hold: prefill_many() packs several slots' rows (2 x S each) into one pass
+        # through the layers, so the weights stream once per batch of utterances instead of once per utterance
+        self.pre_rows = max(2 * self.max_prefill, PREFILL_BATCH_ROWS if self.prefill_batch else 0)
         self.lib = _lib.lib()
         self.stream = torch.cuda.Stream(self.dev)
         self.sptr = self.stream.cuda_stream
@@ -179,7 +184,7 @@ class HipEngine:
             self.row_pos = torch.full((R,), -1, dtype=torch.int32, device=dev)  # every row inactive
             self.kc = z(self.n_kv, R, self.Hkv, self.smax, self.hd)   # K  [layer][row][kv head][position][hd]
             self.vc = z(self.n_kv, R, self.Hkv, self.hd, self.smax)   # V^T [layer][row][kv head][hd][position]
-            nq = max(R, 2 * self.max_prefill)
+            nq = max(R, self.pre_rows)
             wb = self.lib.zmi_attention_work_bytes(nq, self.H, self.Hkv, self.hd, self.smax - 1)
             if wb < 0:
                 raise ValueError("attention geometry not supported by the HIP kernel")
@@ -203,19 +208,19 @@ class HipEngine:
             # zmi_attn_ffn_block hand-off granules (the attention output rows), one area per layer
             self.attn_gran = z(self.L, R, self.lib.zmi_attn_ffn_gran_words(1), dt=torch.int64)
             # zmi_gemv_splitk's fp32 segment sums (fc2 over many rows: decode and prefill)
-            self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, 2 * self.max_prefill), d), dt=torch.float32)
+            self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
                        ("active", "pos", "offset", "remaining", "stopping", "step", "total_len")}
             self.delayed = torch.full((S, N_CODEBOOKS, self.tcap), 1025, dtype=torch.int32, device=dev)
             self.params = z(S * ctypes.sizeof(_lib.Sampling), dt=torch.uint8)
-            P = self.max_prefill
-            self.x_pre, self.q_pre, self.attn_pre = z(2 * P, d), z(2 * P, qd), z(2 * P, qd)
-            self.xn_pre = z(2 * P, d)  # LayerNorm'd prefill rows
-            self.h_pre = z(2 * P, self.F)
-            self.row_kv_pre = z(2 * P, dt=torch.int32)
-            self.row_pos_pre = z(2 * P, dt=torch.int32)
+            P2 = self.pre_rows
+            self.x_pre, self.q_pre, self.attn_pre = z(P2, d), z(P2, qd), z(P2, qd)
+            self.xn_pre = z(P2, d)  # LayerNorm'd prefill rows
+            self.h_pre = z(P2, self.F)
+            self.row_kv_pre = z(P2, dt=torch.int32)
+            self.row_pos_pre = z(P2, dt=torch.int32)
             self.x_last = z(2, d)
             self.logits_pre = z(2, N_CODEBOOKS, 1026, dt=torch.float32)
             self.rope = rope_table(self.hd).to(dev)
@@ -662,53 +667,99 @@ class HipEngine:
             self._advance(k, s)
 
     # ------------------------------------------------------------------ prefill
-    def prefill(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
-                params: SamplingParams, noise: torch.Tensor | None = None):
-        """_prefill + first sample + frame write (reference model.py:240-264) for one slot."""
-        assert 0 <= slot < self.S
+    def _prefill_check(self, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int) -> int:
         lc = cond.shape[1]
         p = 0 if prefix is None else int(prefix.shape[-1])
         s_len = lc + p + 1
-        total = p + max_new_tokens + 9
         if s_len > self.max_prefill:
             raise ValueError(f"prefill length {s_len} > engine max_prefill {self.max_prefill}")
-        if s_len + max_new_tokens + 8 > self.smax or total > self.tcap:
+        if s_len + max_new_tokens + 8 > self.smax or p + max_new_tokens + 9 > self.tcap:
             raise ValueError("utterance longer than the engine's KV capacity")
         if cond.shape[0] != 2 or cond.shape[2] != self.d:
             raise ValueError("prefix_conditioning must be [2 (cond, uncond), Lc, d_model]")
-        L, d, st = self.lib, self.d, self.st
+        return s_len
+
+    def _prefill_stage(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
+                       params: SamplingParams, off: int, s_len: int):
+        """The slot's sampling parameters, delayed-code buffer and granules, and its 2 x s_len prefill rows
+        (cond, uncond) at row `off` of the prefill buffers (reference model.py:181-196, 240-250)."""
+        assert 0 <= slot < self.S
+        L, d = self.lib, self.d
+        lc = cond.shape[1]
+        p = s_len - lc - 1
+        total = p + max_new_tokens + 9
+        cond = cond.to(self.dev, torch.bfloat16)
+        pr = torch.zeros(N_CODEBOOKS, max(p, 1), dtype=torch.int32, device=self.dev)
+        if p:
+            pr[:, :p] = prefix.reshape(N_CODEBOOKS, p).to(self.dev, torch.int32)
+        cp = torch.tensor(bytearray(params.to_c()), dtype=torch.uint8)
+        sz = ctypes.sizeof(_lib.Sampling)
+        self.params[slot * sz:(slot + 1) * sz].copy_(cp)
+        self.slot_greedy[slot] = params.temperature <= 0
+        _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
+        self._reset_granules(slot)  # no granule of an earlier utterance may match a tag
+        xp = self.x_pre[off: off + 2 * s_len]
+        xp[:lc] = cond[0]
+        xp[s_len: s_len + lc] = cond[1]
+        codes = self.delayed[slot]
+        for half in range(2):
+            _lib.check(L.zmi_embed_codes(codes.data_ptr(), self.tcap, p + 1, self.w["emb"].data_ptr(), d,
+                                         xp[half * s_len + lc].data_ptr(), d, self.sptr), "embed_codes")
+        ar = torch.arange(s_len, dtype=torch.int32, device=self.dev)
+        self.row_pos_pre[off: off + 2 * s_len] = torch.cat([ar, ar])
+        self.row_kv_pre[off: off + s_len] = 2 * slot
+        self.row_kv_pre[off + s_len: off + 2 * s_len] = 2 * slot + 1
+
+    def _prefill_finish(self, slot: int, max_new_tokens: int, off: int, s_len: int, p: int, noise):
+        """Heads of the slot's last prefill rows, slot state, first sample + frame write (model.py:251-264)."""
+        self._prefill_logits(s_len) if off == 0 else self._prefill_logits(s_len, off)
+        vals = {"active": 1, "pos": s_len, "offset": p, "remaining": max_new_tokens + 8, "stopping": 0,
+                "step": 0, "total_len": p + max_new_tokens + 9}
+        for k, v in vals.items():
+            self.st[k][slot] = v
+        self._sample(self.logits_pre, noise, 1, slot, 1)
+        self.pos_hi[slot] = s_len
+
+    def prefill(self, slot: int, cond: torch.Tensor, prefix: torch.Tensor | None, max_new_tokens: int,
+                params: SamplingParams, noise: torch.Tensor | None = None):
+        """_prefill + first sample + frame write (reference model.py:240-264) for one slot."""
+        s_len = self._prefill_check(cond, prefix, max_new_tokens)
+        p = s_len - cond.shape[1] - 1
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.stream):
-            cond = cond.to(self.dev, torch.bfloat16)
-            pr = torch.zeros(N_CODEBOOKS, max(p, 1), dtype=torch.int32, device=self.dev)
-            if p:
-                pr[:, :p] = prefix.reshape(N_CODEBOOKS, p).to(self.dev, torch.int32)
-            cp = torch.tensor(bytearray(params.to_c()), dtype=torch.uint8)
-            sz = ctypes.sizeof(_lib.Sampling)
-            self.params[slot * sz:(slot + 1) * sz].copy_(cp)
-            self.slot_greedy[slot] = params.temperature <= 0
-            _lib.check(L.zmi_delay_init(ctypes.byref(self.slots), slot, pr.data_ptr(), p, total, self.sptr), "delay")
-            self._reset_granules(slot)  # no granule of an earlier utterance may match a tag
-            xp = self.x_pre[: 2 * s_len]
-            xp[:lc] = cond[0]
-            xp[s_len: s_len + lc] = cond[1]
-            codes = self.delayed[slot]
-            for half in range(2):
-                _lib.check(L.zmi_embed_codes(codes.data_ptr(), self.tcap, p + 1, self.w["emb"].data_ptr(), d,
-                                             xp[half * s_len + lc].data_ptr(), d, self.sptr), "embed_codes")
-            ar = torch.arange(s_len, dtype=torch.int32, device=self.dev)
-            self.row_pos_pre[: 2 * s_len] = torch.cat([ar, ar])
-            self.row_kv_pre[:s_len] = 2 * slot
-            self.row_kv_pre[s_len: 2 * s_len] = 2 * slot + 1
+            self._prefill_stage(slot, cond, prefix, max_new_tokens, params, 0, s_len)
             self._prefill_layers(2 * s_len, s_len - 1)
-            self._prefill_logits(s_len)
-            vals = {"active": 1, "pos": s_len, "offset": p, "remaining": max_new_tokens + 8, "stopping": 0,
-                    "step": 0, "total_len": total}
-            for k, v in vals.items():
-                st[k][slot] = v
-            self._sample(self.logits_pre, noise, 1, slot, 1)
-        self.pos_hi[slot] = s_len
+            self._prefill_finish(slot, max_new_tokens, 0, s_len, p, noise)
         return s_len
+
+    def prefill_many(self, items) -> list:
+        """prefill() of several slots: items are (slot, cond, prefix, max_new_tokens, params). Their rows are
+        packed into passes of up to `pre_rows` rows, each pass through the layers once (one weight stream for
+        all of them). Every kernel's per-row arithmetic is independent of the rows beside it (the GEMV / GEMM /
+        split-K forms and the attention are tested batch-invariant), so each slot decodes exactly as if it had
+        been prefilled alone (generate_batch == generate)."""
+        items = list(items)
+        if not self.prefill_batch or len(items) <= 1:
+            return [self.prefill(*it) for it in items]
+        lens = [self._prefill_check(it[1], it[2], it[3]) for it in items]
+        groups, cur, rows = [], [], 0
+        for it, s_len in zip(items, lens):
+            if cur and rows + 2 * s_len > self.pre_rows:
+                groups.append(cur)
+                cur, rows = [], 0
+            cur.append((it, s_len, rows))
+            rows += 2 * s_len
+        groups.append(cur)
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.stream):
+            for g in groups:
+                for (slot, cond, prefix, mnt, params), s_len, off in g:
+                    self._prefill_stage(slot, cond, prefix, mnt, params, off, s_len)
+                m = g[-1][2] + 2 * g[-1][1]
+                self._prefill_layers(m, max(s_len for _, s_len, _ in g) - 1)
+                for (slot, cond, prefix, mnt, params), s_len, off in g:
+                    self._prefill_finish(slot, mnt, off, s_len, s_len - cond.shape[1] - 1, None)
+        return lens
 
     def _reset_granules(self, slot: int):
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
@@ -719,11 +770,12 @@ class HipEngine:
             self.eng_gran.zero_()
             self.lay_gran.zero_()
 
-    def _prefill_logits(self, s_len: int):
-        """Heads of the last position of the cond / uncond prefill rows -> logits_pre (model.py:103-116)."""
+    def _prefill_logits(self, s_len: int, off: int = 0):
+        """Heads of the last position of the cond / uncond prefill rows (starting at row `off`) -> logits_pre
+        (model.py:103-116)."""
         xp = self.x_pre
-        self.x_last[0] = xp[s_len - 1]
-        self.x_last[1] = xp[2 * s_len - 1]
+        self.x_last[0] = xp[off + s_len - 1]
+        self.x_last[1] = xp[off + 2 * s_len - 1]
         self._run_gemv(self._gemv(self.w["heads"], self.x_last, 2, HEADS_N_PAD, self.d, _lib.EPI_LOGITS,
                                   self.logits_pre, 0, n_valid=HEADS_N, ln=(self.w["nf_w"], self.w["nf_b"])))
 

@@ -49,6 +49,8 @@ def neox_pair_perm(hd: int) -> torch.Tensor:
 class HybridEngine(HipEngine):
     hybrid = True
 
+    prefill_batch = False  # the Mamba2 prefill scan takes one (cond, uncond) pair of sequences per pass
+
     def __init__(self, cfg, device="cuda", max_slots: int = 1, max_seqlen: int = 2048, max_prefill: int = 512):
         bb = cfg.backbone
         if bb.rms_norm or bb.residual_in_fp32:

@@ -176,13 +176,15 @@ class Zonos:
         remaining = [0] * slots
 
         def fill():
+            items = []
             for s in range(slots):
                 if owner[s] < 0 and queue:
                     i = queue.pop(0)
                     params = SamplingParams.from_dict(dict(sampling_params), cfg_scale, seeds[i])
-                    e.prefill(s, conds[i], prefixes[i], mnt[i], params)
+                    items.append((s, conds[i], prefixes[i], mnt[i], params))
                     owner[s] = i
                     remaining[s] = mnt[i] + 8
+            e.prefill_many(items)  # the free slots' prefills in as few passes through the layers as fit
 
         fill()
         while any(o >= 0 for o in owner):
