@@ -41,32 +41,70 @@ def cond_tensor(seed: int, d: int, dev, lc: int = LC):
     return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
 
 
-def time_dominant_kernel(model, reps: int = 3):
-    """The largest kernel of the C2 step, the fc1 GEMV (LayerNorm prologue + packed SwiGLU epilogue: 67.1 MB of
-    weights per launch), for every layer, timed with HIP events on the engine stream: the 26 layers' launches
-    back to back, `reps` times. Rotating over all 26 layers' weights (1.7 GB) keeps the stream out of the
-    256 MiB Infinity Cache, so the bytes come from HBM as in the decode step. Returns (us per launch,
-    algorithmic bytes)."""
+def engine_bytes(e, pos: int, nxt: int = 0) -> int:
+    """Algorithmic HBM bytes of one zmi_layer_engine launch: the layer's out_proj, fc1 and fc2 weights, the next
+    op's weights (QKV of the next layer, or the heads), this layer's K / V of both CFG rows up to pos, the
+    next layer's K / V row written at pos."""
+    d, F = e.d, e.F
+    qkv_n = (e.H + 2 * e.Hkv) * e.hd
+    w = (d * d + 2 * F * d + d * F) * 2 + (qkv_n * d * 2 if nxt == 0 else 9248 * d * 2)
+    kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)
+    return w + kv + (2 * 2 * e.Hkv * e.hd * 2 if nxt == 0 else 0)
+
+
+def _live_state(model, cond):
+    """Prefill slot 0 with the bench conditioning and decode to the C2 mean position; returns the position."""
+    from zonos_vibes_amd.engine import SamplingParams
     e = model.engine
-    items = [item for kind, item in e._plan(2) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
-    assert items, "the C2 plan has no fc1 GEMV launch"
+    s_len = e.prefill(0, cond, None, N_NEW, SamplingParams(temperature=0.0, cfg_scale=2.0))
+    lead = (N_NEW + 8) // 2
+    e.step(lead, slots=1)
+    return s_len + lead
+
+
+def time_dominant_kernel(model, cond, reps: int = 3):
+    """The dominant kernel of the C2 step, timed with HIP events on the engine stream inside this run.
+    Engine plan: zmi_layer_engine with the next layer's QKV (layer_engine_kernel<0>: 121.6 MB of weights + the
+    layer's K / V per launch), layers 0..24 back to back at the C2 mean position, every layer's hand-off granules
+    zeroed before each pass (outside the events). Launch plan: the fc1 GEMV (LayerNorm prologue + SwiGLU
+    epilogue, 67.1 MB). The 26 layers' weights (3.2 GB) rotate, so the bytes come from HBM as in the decode step.
+    Returns (us per launch, algorithmic bytes per launch, kernel name)."""
+    e = model.engine
+    pos = _live_state(model, cond)
+    form = e._segments(1, 1)[0][1]
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     tot = 0.0
-    with torch.cuda.stream(e.stream):
-        for r in range(reps + 1):
-            st.record(e.stream)
+    if form == "engine":
+        items = [it for kind, it in e._plan(2, form) if kind == "layereng" and it.next == 0]
+
+        def run():
+            for it in items:
+                _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
+        bytes_launch, name = engine_bytes(e, pos), "layer_engine_kernel<0>"
+    else:
+        items = [item for kind, item in e._plan(2, form) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
+        assert items, "the C2 plan has no fc1 GEMV launch"
+
+        def run():
             for it in items:
                 e._run_gemv(it)
+        d, F = e.d, e.F
+        bytes_launch, name = 2 * F * d * 2 + 2 * d * 2 + 2 * d * 2 + 2 * F * 2, "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"
+    with torch.cuda.stream(e.stream):
+        for r in range(reps + 1):
+            e.lay_gran.zero_()
+            st.record(e.stream)
+            run()
             en.record(e.stream)
             en.synchronize()
             if r:
                 tot += st.elapsed_time(en) * 1000.0
-    d, F = e.d, e.F
-    bytes_launch = 2 * F * d * 2 + 2 * d * 2 + 2 * d * 2 + 2 * F * 2  # weights, x rows in, ln gamma / beta, h out
-    return tot / (reps * len(items)), bytes_launch
+    e.check_errors()
+    e.release(0)
+    return tot / (reps * len(items)), bytes_launch, name
 
 
-DOMINANT_KERNEL = "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"
+DOMINANT_KERNEL = "layer_engine_kernel<0>"
 
 
 def _time_fused(e, items, gran, run, reps: int) -> float:
@@ -88,7 +126,7 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
     return tot / (reps * len(items))
 
 
-PMC_FILE = "r03c_pmc_fc1_fetch.json"
+PMC_FILE = "r04_pmc_engine_fetch.json"
 
 
 def pmc_traffic():
@@ -146,6 +184,8 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     plan = e._plan(2, form)
     d, F, qkv_n = e.d, e.F, (e.H + 2 * e.Hkv) * e.hd
     kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)  # K + V of both CFG rows, one layer
+    if form == "engine":
+        return _engine_kernel_table(e, plan, pos, reps)
     gem = [it for kd, it in plan if kd == "gemv"]
     res = [it for it in gem if it[1] == _lib.EPI_RESIDUAL]
     fused_ffn = any(kd == "ffnblk" for kd, _ in plan)
@@ -208,6 +248,66 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     e.check_errors()
     e.release(0)
     return {"pos": pos, "kernels": out}
+
+
+def _sampler_us(e, reps: int) -> tuple[float, str]:
+    """The sampler launches captured in one graph (a Python-side launch costs more than the kernel, so
+    back-to-back launches from the host would time the host)."""
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n_s = 8 * reps
+    _lib.check(e.lib.zmi_graph_begin(e.sptr), "graph_begin")
+    try:
+        for _ in range(n_s):
+            e._sample(e.logits, None, 0, 0, 1)
+    finally:
+        g = ctypes.c_void_p()
+        _lib.check(e.lib.zmi_graph_end(e.sptr, ctypes.byref(g)), "graph_end")
+    _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")  # warm
+    st.record(e.stream)
+    _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")
+    en.record(e.stream)
+    en.synchronize()
+    _lib.check(e.lib.zmi_graph_destroy(g.value))
+    kind = "greedy: one workgroup per slot" if e._greedy_step(0, 1) else "per-codebook workgroups"
+    return st.elapsed_time(en) * 1000.0 / n_s, kind
+
+
+def _engine_kernel_table(e, plan, pos: int, reps: int) -> dict:
+    """kernel_table for the engine plan: layer 0's QKV GEMV, the 25 layer-engine launches that end with the next
+    layer's QKV, the last one (norm_f + heads), the sampler; each layer's granules zeroed before a pass."""
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {}
+    qkv0 = [it for kd, it in plan if kd == "gemv"]
+    eng = [it for kd, it in plan if kd == "layereng"]
+    kinds = {"qkv layer 0 (gemv: LN + QKV + RoPE + KV write)": (lambda it: e._run_gemv(it), qkv0,
+                                                                  (e.H + 2 * e.Hkv) * e.hd * e.d * 2),
+             "layer_engine<0> (attention + out_proj + fc1 + fc2 + next LN/QKV)":
+                 (lambda it: _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 0],
+                  engine_bytes(e, pos, 0)),
+             "layer_engine<1> (attention + out_proj + fc1 + fc2 + norm_f + heads)":
+                 (lambda it: _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 1],
+                  engine_bytes(e, pos, 1))}
+    with torch.cuda.stream(e.stream):
+        for name, (run, items, nbytes) in kinds.items():
+            tot = 0.0
+            for r in range(reps + 1):
+                e.lay_gran.zero_()
+                st.record(e.stream)
+                for it in items:
+                    run(it)
+                en.record(e.stream)
+                en.synchronize()
+                if r:
+                    tot += st.elapsed_time(en) * 1000.0
+            us = tot / (reps * len(items))
+            out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
+                             hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items))
+        us, kind = _sampler_us(e, reps)
+        out[f"sampler (CFG + penalty + argmax + FSM + next embedding; {kind})"] = dict(
+            us=round(us, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
+    e.check_errors()
+    e.release(0)
+    return {"pos": pos, "form": "engine", "kernels": out}
 
 
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA
@@ -710,7 +810,7 @@ def main():
             gather = {"ok": False, "error": f"{type(exc).__name__}: {exc}"[:200]}
 
     # kernel-level measurement (outside the timed region)
-    us, bl = time_dominant_kernel(model)
+    us, bl, dom_name = time_dominant_kernel(model, cond)
     step_us, step_pos = time_decode_step(model, cond)
     ktab = kernel_table(model, cond)
     widened = time_widened_rows(model, dev)
@@ -744,8 +844,9 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": "gemv_kernel<2, 4, 8, 16, 1, 3, 1> (fc1: LayerNorm prologue + packed SwiGLU "
-                                   "epilogue, 67.1 MB bf16 weights per launch)",
+            "roofline": {"kernel": dom_name + (" (one whole decode layer + the next layer's QKV: 121.6 MB bf16 weights "
+                                                "+ the layer's K / V per launch)" if "engine" in dom_name else
+                                                " (fc1: LayerNorm prologue + packed SwiGLU epilogue, 67.1 MB)"),
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
                          "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2, bytes/launch)",

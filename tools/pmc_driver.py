@@ -7,8 +7,10 @@ C2 mean position, on the synthetic Zonos-v0.1 engine (B = 1, two CFG rows).
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attn        (and WRITE_SIZE)
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention)
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py ffnblk      (fused out_proj + fc1)
+    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py engine      (zmi_layer_engine, layers 0..24)
 then tools/pmc_summary.py turns the counter CSV into the per-launch JSON kept under profiles/.
 """
+import ctypes
 import os
 import sys
 
@@ -30,6 +32,7 @@ def main(which: str, reps: int = 2):
         e.row_pos[:2] = POS
         e.row_kv[:2] = torch.arange(2, dtype=torch.int32, device=dev)
         e.x.normal_()
+        e.q.normal_()
         e.kc.normal_()
         e.vc.normal_()
     e.stream.synchronize()
@@ -39,6 +42,9 @@ def main(which: str, reps: int = 2):
         e._build_plan()
     if which == "ffnblk":  # the fused out_proj + fc1 launch (off by default)
         e.ffn_block = True
+        e._build_plan()
+    if which != "engine":
+        e.layer_engine = False  # the launch plan's kernels
         e._build_plan()
     plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
     for _ in range(reps):
@@ -59,6 +65,11 @@ def main(which: str, reps: int = 2):
             for kind, it in plan:
                 if kind == "attnblk":
                     e._run_attn_block(it)
+        elif which == "engine":  # the layer engine launches with the next layer's QKV (granules fresh per rep)
+            e.lay_gran.zero_()
+            for kind, it in plan:
+                if kind == "layereng" and it.next == 0:
+                    _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
         else:
             raise SystemExit(f"unknown driver {which}")
     e.stream.synchronize()
