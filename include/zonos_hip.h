@@ -434,11 +434,18 @@ int zmi_version(void);
  *   ZMI_OPT_AF_DEPTH (default 3): weight loads each streaming wave of zmi_attn_ffn_block keeps in flight (1 KiB
  *          each; 2, 3, 4, 6 or 0 = unthrottled): the launch's latency-bound hand-offs queue behind whatever the
  *          chip has in flight, so the weight stream is issued progressively.
- *   ZMI_OPT_ENG_START (default 1): how zmi_ffn_engine's ring starts: 0 = every slot at once, 1 = the out_proj slot
- *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
- *   ZMI_OPT_ENG_SPARE: reserved for engine experiments (0). */
+ *   ZMI_OPT_ENG_FLY (default 8): weight-ring slots (8 KiB) zmi_layer_engine's loader wave keeps in flight (1..8);
+ *   ZMI_OPT_ENG_THIN (default 2): the same while a service wave of the CU polls a hand-off (1..ENG_FLY).
+ *   ZMI_OPT_ENG_HOLD (default 1): zmi_layer_engine's attention-chunk workgroups issue no weights until their K / V
+ *          landed.
+ *   ZMI_OPT_ENG_PF (default 1): zmi_layer_engine's prefetch wave warms the Infinity Cache with the workgroup's
+ *          later weight slots during the attention phase.
+ *   ZMI_OPT_ENG_DELAY (default 0): ns the non-attention workgroups' weight loaders wait at launch start.
+ *   ZMI_OPT_ENG_START (default 1): how zmi_ffn_engine's rings start: 0 = every slot at once, 1 = the out_proj slot
+ *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
-       ZMI_OPT_ENG_SPARE = 5, ZMI_OPT_COUNT = 6 };
+       ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
+       ZMI_OPT_COUNT = 10 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

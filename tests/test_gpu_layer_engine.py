@@ -32,7 +32,7 @@ def _state(e):
 def test_layer_engine_step_bit_identical(lc, steps):
     """Teacher-forced decode steps from one prefill, engine plan against the launch plan, at positions that
     start a 128-key chunk, cross a 512-key softmax block and pass the fused attention forms' reach (1023)."""
-    m = _model(3, lc, 16)
+    m = _model(3, lc, 48)
     e = m.engine
     cond = _cond(11, lc, 2048).to(DEV)
     from zonos_vibes_amd.engine import SamplingParams
@@ -41,6 +41,9 @@ def test_layer_engine_step_bit_identical(lc, steps):
     for use in (False, True):
         e.layer_engine = use
         e._build_plan()
+        with torch.cuda.stream(e.stream):  # positions past the prefill must not hold the other run's steps
+            e.kc.zero_()
+            e.vc.zero_()
         e.prefill(0, cond, None, 40, params)
         states = []
         for _ in range(steps):
@@ -69,4 +72,6 @@ def test_layer_engine_generate_codes_equal():
     e._build_plan()
     got = m.generate(cond, max_new_tokens=80, sampling_params=params, progress_bar=False)
     assert any(k[1] == "engine" for k in e._graphs), sorted(e._graphs)
+    e.layer_engine = False
+    e._build_plan()
     assert torch.equal(got, ref)

@@ -22,7 +22,11 @@ OPT_GEMM_ROWS = 1
 OPT_AF_DEPTH = 2
 OPT_AF_DELAY = 3
 OPT_ENG_START = 4
-OPT_ENG_SPARE = 5
+OPT_ENG_FLY = 5
+OPT_ENG_THIN = 6
+OPT_ENG_HOLD = 7
+OPT_ENG_PF = 8
+OPT_ENG_DELAY = 9
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3

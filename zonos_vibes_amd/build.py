@@ -50,10 +50,12 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     for p in procs:
         _wait(p)
     if force or _stale(lib, objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", lib]
+        tmp = lib + ".tmp"  # linked aside, then renamed: a reader never sees a half-written library
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", tmp]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
+        os.replace(tmp, lib)
     return lib
 
 

@@ -123,4 +123,30 @@ __device__ __forceinline__ void ln_row(bf16_t* xr, const bf16_t* gw, const bf16_
     *reinterpret_cast<uint4*>(xr + q * 512 + lane * 8) = ln_apply(xv[q], gv[q], bv[q], rstd, nbias);
 }
 
+// ln_row with the LayerNorm weight / bias chunks of the lane already in registers (gw[q] = w[q 512 + 8 lane ..])
+__device__ __forceinline__ void ln_row_r(bf16_t* xr, const uint4 (&gv)[4], const uint4 (&bv)[4], float eps, int lane) {
+  constexpr int NQ = 4, K = 2048;
+  uint4 xv[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) xv[q] = *reinterpret_cast<const uint4*>(xr + q * 512 + lane * 8);
+  float part[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    float t = 0.f;
+    t += ln_chunk_sum(xv[q], 0.f, false);
+    part[q] = wave_sum(t);
+  }
+  const float mean = ln_combine<NQ>(part) / (float)K;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    float t = 0.f;
+    t += ln_chunk_sum(xv[q], mean, true);
+    part[q] = wave_sum(t);
+  }
+  const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part) / (float)K + eps), nbias = -mean * rstd;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    *reinterpret_cast<uint4*>(xr + q * 512 + lane * 8) = ln_apply(xv[q], gv[q], bv[q], rstd, nbias);
+}
+
 }  // namespace zmi_eng

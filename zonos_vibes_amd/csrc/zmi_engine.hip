@@ -340,7 +340,7 @@ extern "C" int zmi_ffn_engine(const ZmiFfnEngineArgs* args, void* stream) {
   a.err = e.err;
   a.diag = (unsigned long long*)e.diag;
   a.start = zmi_option(ZMI_OPT_ENG_START);
-  a.spare = zmi_option(ZMI_OPT_ENG_SPARE);
+  a.spare = 0;
   hipLaunchKernelGGL(ffn_engine_kernel, dim3(NBLK), dim3(NT), L_BYTES, (hipStream_t)stream, a);
   ZMI_CHECK(hipGetLastError());
   return 0;

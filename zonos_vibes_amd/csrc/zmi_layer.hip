@@ -45,18 +45,21 @@ using zmi_attn::HD;
 using zmi_attn::mfma16;
 
 constexpr int DM = 2048, FF = 8192, XG = 4, HKV = 4, QCOLS = 2048, KCOLS = 512;
-constexpr int NBLK = 256, NCW = 4, NSW = 4, NWV = NCW + NSW, NT = NWV * 64;
+constexpr int NBLK = 256, NLW = 2, NCW = 4, NSW = 4, NPW = 1, NWV = NLW + NCW + NSW + NPW, NT = NWV * 64;
+constexpr int CPL = NCW / NLW;  // consumers per loader wave
+constexpr int MAXFLY = 8;  // ring slots the loader may keep in flight (its vmcnt waits encode up to 8 x 7 pieces)
 constexpr int MAXR = 2, DEPTH = 4;
 constexpr int NCH = 32;                 // chunk blocks per attention unit: positions < NCH x CH = 4096
 constexpr int NUNIT = 8;                // (row, kv head) units
-constexpr int MDIM = HD / NCH;          // output dims merged per chunk block
+constexpr int NMRG = 8;                 // chunk blocks 0..7 of a unit merge its output, 16 dims each
+constexpr int MDIM = HD / NMRG;
 constexpr int CPG = CH / 32;            // 32-key groups per chunk
 constexpr int NEXT_QKV = 0, NEXT_HEADS = 1;
 constexpr int HEADS_GROUPS = 9248 / 8, HEADS_VALID = 9 * 1026 - 0;  // 9 x 1026 columns (1025 real + pad row each)
 constexpr int MAXNEXT = 5;
 constexpr int NSLOT_MAX = 13 + MAXNEXT;
 constexpr int XROW = DM + 8;
-static_assert(NCH * NUNIT == NBLK && CPG == 4 && MDIM == 4, "geometry");
+static_assert(NCH * NUNIT == NBLK && CPG == 4 && MDIM == 16, "geometry");
 
 // granule areas (u64 words) of one layer for M rows
 struct Gran {
@@ -82,8 +85,9 @@ constexpr size_t L_BUFB = L_BUFA + (size_t)MAXR * XROW * 2;              // bf16
 constexpr size_t L_REDO = L_BUFB + (size_t)MAXR * XROW * 2;              // f32 [NCW][8][MAXR]
 constexpr size_t L_REDF = L_REDO + (size_t)NCW * 8 * MAXR * 4;           // f32 [8][NCW][8][MAXR]
 constexpr size_t L_REDN = L_REDF + (size_t)8 * NCW * 8 * MAXR * 4;       // f32 [MAXNEXT][NCW][8][MAXR]
-constexpr size_t L_CNT = L_REDN + (size_t)MAXNEXT * NCW * 8 * MAXR * 4;  // u32 [16]
-constexpr size_t L_BYTES = L_CNT + 16 * 4;
+constexpr size_t L_CNT = L_REDN + (size_t)MAXNEXT * NCW * 8 * MAXR * 4;  // u32 [64]
+constexpr size_t L_SINK = L_CNT + 64 * 4;                                  // 1 KiB landing area of the prefetch wave
+constexpr size_t L_BYTES = L_SINK + 1024;
 // the attention scratch lives in BUFA + BUFB (free until the attention output is gathered)
 constexpr size_t A_SC = L_BUFA;                                          // f32 [XG][CH] scores
 constexpr size_t A_PB = A_SC + (size_t)XG * CH * 4;                      // bf16 [XG][CH] P
@@ -92,7 +96,13 @@ constexpr size_t A_MJ = A_OP + (size_t)CPG * XG * HD * 4;                // f32 
 static_assert(A_MJ + 16 <= L_REDO, "attention scratch");
 static_assert(L_BYTES <= 160 * 1024, "LDS");
 static_assert(L_BUFA % 16 == 0 && L_BUFB % 16 == 0 && L_CNT % 16 == 0, "alignment");
-enum { C_READY = 0, C_SVC = 1, C_O = 2, C_F1 = 3, C_N = 11 };  // C_F1 + j (j < 8), C_N + i (i < MAXNEXT)
+// C_F1 + j (j < 8), C_N + i (i < MAXNEXT); C_FULL / C_FREE + c DEPTH + ring slot: k + 1 once slot k of consumer c
+// has landed / been read; C_THIN > 0 while a service wave polls (the loader then keeps few slots in flight)
+// C_HOLD: nonzero while this block's attention chunk still loads its K / V (the loaders issue nothing then)
+// C_PFGO / C_PFSTOP: the prefetch wave may start / must stop
+enum { C_READY = 0, C_SVC = 1, C_O = 2, C_F1 = 3, C_N = 11, C_THIN = 16, C_FULL = 17, C_FREE = 33, C_HOLD = 49,
+       C_PFGO = 50, C_PFSTOP = 51, C_WORDS = 52 };
+static_assert(C_WORDS <= 64, "LDS words");
 
 struct LArgs {
   const char* w_out;
@@ -118,11 +128,14 @@ struct LArgs {
   uint64_t* gran;
   unsigned* err;
   unsigned long long* diag;
-  int start, spare;
+  int fly, thin;  // ZMI_OPT_ENG_FLY / ZMI_OPT_ENG_THIN: slots per loader in flight, and while a service wave polls
+  int hold;       // ZMI_OPT_ENG_HOLD: attention-chunk blocks issue no weights until their K / V landed
+  int pf;         // ZMI_OPT_ENG_PF: the prefetch wave warms the Infinity Cache with the block's later slots
+  int delay;      // ZMI_OPT_ENG_DELAY: ns the other blocks' loaders wait at launch start
 };
 
 __device__ __forceinline__ void stamp(const LArgs& a, int i) {
-  if (a.diag && (threadIdx.x & 63) == 0) a.diag[(size_t)blockIdx.x * 32 + i] = __builtin_amdgcn_s_memrealtime();
+  if (a.diag && (threadIdx.x & 63) == 0) a.diag[(size_t)blockIdx.x * 64 + i] = __builtin_amdgcn_s_memrealtime();
 }
 
 __device__ __forceinline__ lds_u32* cnt(char* smem, int i) { return lds_word(smem, L_CNT + 4 * i); }
@@ -146,17 +159,106 @@ __device__ __forceinline__ const char* slot_src(const LArgs& a, int k, int b, in
   return a.w_next + ((size_t)(b + 256 * (k - 13)) * 32 + c * 8) * 1024;
 }
 
+__device__ __forceinline__ unsigned lds_ld(char* smem, int i) {
+  return __hip_atomic_load(cnt(smem, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(char* smem, int i, unsigned v) {
+  __hip_atomic_store(cnt(smem, i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// the oldest of `n + 1` outstanding slots has landed (loads complete in order)
+__device__ __forceinline__ void wait_oldest(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+  }
+}
+static_assert(MAXFLY <= 8, "wait_oldest encodes up to 7 slots issued after the awaited one");
+
+// The loader wave: every consumer's slots in (slot, consumer) order through the consumers' rings, by
+// non-temporal LDS-DMA; slot k of consumer c is published FULL once landed and re-filled once the consumer
+// marked it FREE. It keeps `a.fly` slots in flight, `a.thin` while a service wave of the block polls
+// (MI355X_MICROARCH.md gather-pass: a poll queues behind the CU's own refill burst). It issues nothing
+// else, so its vmcnt counts exactly its DMA pieces.
+template <int NEXT>
+__device__ __forceinline__ void loader(const LArgs& a, char* smem, int b, int lw, int lane) {
+  const unsigned ring0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) char*)(smem + L_RING));
+  const int ns = CPL * (13 + n_next<NEXT>(b));
+  if (a.delay > 0) {  // let the attention chunks' K / V loads reach HBM ahead of the weight streams
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(a.delay / 10);
+    while (__builtin_amdgcn_s_memrealtime() < t_end) __builtin_amdgcn_s_sleep(2);
+  }
+  int issued = 0, landed = 0;
+  for (unsigned spin = 0; landed < ns;) {
+    while (issued < ns) {
+      const int k = issued / CPL, c = lw * CPL + (issued - k * CPL);
+      const int lim = lds_ld(smem, C_HOLD) ? 0 : (lds_ld(smem, C_THIN) ? a.thin : a.fly);
+      if (issued - landed >= lim) break;
+      if (k >= DEPTH && lds_ld(smem, C_FREE + c * DEPTH + k % DEPTH) < (unsigned)(k - DEPTH + 1)) break;
+      issue_slot(slot_src<NEXT>(a, k, b, c), ring0 + (c * DEPTH + k % DEPTH) * SLOT, lane);
+      if (c == NCW - 1 && (k == 0 || k == 1 || k == 4 || k == 8 || k == 9 || k == 12 || k == 13)) stamp(a, 40 + (k < 2 ? k : (k == 4 ? 2 : (k == 8 ? 3 : (k == 9 ? 4 : (k == 12 ? 5 : 6))))));
+      ++issued;
+    }
+    if (issued > landed) {
+      wait_oldest(issued - landed - 1);
+      const int k = landed / CPL, c = lw * CPL + (landed - k * CPL);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) lds_st(smem, C_FULL + c * DEPTH + k % DEPTH, (unsigned)(k + 1));
+      if (c == NCW - 1 && (k == 0 || k == 8 || k == 12)) stamp(a, 48 + (k == 0 ? 0 : (k == 8 ? 1 : 2)));
+      ++landed;
+      spin = 0;
+    } else {  // nothing in flight and nothing issuable: a consumer has not freed its slot yet
+      if (++spin > SPIN) {
+        give_up(a.err);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The prefetch wave: default-policy LDS-DMA reads (into a 1 KiB sink) of the block's weight slots past the
+// loaders' first ring fill, in stream order, while the block waits on the attention chain (HBM is otherwise
+// idle then); the loaders' later reads of those slots hit the Infinity Cache. It starts once C_PFGO is set
+// and stops at C_PFSTOP (before the block's first latency-critical gather of its own), at most 40 KiB in flight.
+template <int NEXT>
+__device__ __forceinline__ void prefetcher(const LArgs& a, char* smem, int b, int lane) {
+  if (!a.pf) return;
+  const unsigned sink = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) char*)(smem + L_SINK));
+  for (unsigned spin = 0; !lds_ld(smem, C_PFGO); ++spin) {
+    if (lds_ld(smem, C_PFSTOP) || spin > SPIN) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  const int ns = NCW * (13 + n_next<NEXT>(b));
+  for (int t = NCW * DEPTH; t < ns; ++t) {
+    if (lds_ld(smem, C_PFSTOP)) break;
+    const int k = t / NCW, c = t - k * NCW;
+    const char* g = slot_src<NEXT>(a, k, b, c) + lane * 16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(g + j * 1024), "s"(sink)
+                   : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int NEXT>
 __device__ __forceinline__ void consumer(const LArgs& a, char* smem, int b, int c, int lane, const unsigned (&tag)[MAXR]) {
-  const unsigned ring = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) char*)(smem + L_RING + (size_t)c * DEPTH * SLOT));
   const int nslot = 13 + n_next<NEXT>(b);
-  // out_proj's slot first (it is on the critical path after the attention); with start 1 it has landed
-  // before the fc1 slots are requested
-  issue_slot(slot_src<NEXT>(a, 0, b, c), ring, lane);
-  if (a.start == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int k = 1; k < DEPTH; ++k) issue_slot(slot_src<NEXT>(a, k, b, c), ring + k * SLOT, lane);
   const bf16_t* bufA = reinterpret_cast<const bf16_t*>(smem + L_BUFA);
   const bf16_t* bufB = reinterpret_cast<const bf16_t*>(smem + L_BUFB);
   float* redo = reinterpret_cast<float*>(smem + L_REDO);
@@ -164,50 +266,54 @@ __device__ __forceinline__ void consumer(const LArgs& a, char* smem, int b, int 
   float* redn = reinterpret_cast<float*>(smem + L_REDN);
   const int s = b & 7, m = b >> 3;
   const int col = lane & 15, quad = lane >> 4;
-  uint4 xa0[16], xa1[16];
-  auto load_frag = [&](const bf16_t* buf, int koff, int nch) {  // gemv_body step 4's A operand
-    const int ar = min(col, a.M - 1);
-    const bf16_t* p = buf + ar * XROW + koff + quad * 8;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j < nch) {
-        xa0[j] = *reinterpret_cast<const uint4*>(p + j * 64);
-        xa1[j] = *reinterpret_cast<const uint4*>(p + j * 64 + 32);
-      }
-  };
+  const int ar = min(col, a.M - 1);
   f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < NSLOT_MAX; ++k) {
     if (k >= 13 && k >= nslot) continue;  // blocks with fewer next-op slots (compile-time trip count: unrolled)
-    if (k == 0) {
+    if (k == 0)
       lds_wait_ge(cnt(smem, C_READY), NSW * 1, a.err);
-      load_frag(bufA, c * 512, 8);
-    } else if (k == 1) {
+    else if (k == 1)
       lds_wait_ge(cnt(smem, C_READY), NSW * 2, a.err);
-      load_frag(bufB, c * 512, 8);
-    } else if (k == 9) {
+    else if (k == 9)
       lds_wait_ge(cnt(smem, C_READY), NSW * 3, a.err);
-      load_frag(bufA, 0, 16);
-    } else if (k == 13) {
+    else if (k == 13)
       lds_wait_ge(cnt(smem, C_READY), NSW * 4, a.err);
-      load_frag(bufB, c * 512, 8);
+    // this item's activation rows (gemv_body step 4's A operand: lane l reads row min(l & 15, M - 1), k =
+    // 8 (l >> 4) .. + 7 of each 32-wide k-half), read per chunk from LDS
+    const bool f2 = k >= 9 && k <= 12;
+    const bool second = f2 && ((k - 9) & 1);  // second half of an fc2 segment: the chain continues
+    const bf16_t* xb = (k == 0 || f2 ? bufA : bufB) + ar * XROW + (f2 ? 8 * 64 * (second ? 1 : 0) : c * 512) + quad * 8;
+    // the slot: landed (FULL), read, then FREE for the loader
+    {
+      lds_u32* full = cnt(smem, C_FULL + c * DEPTH + k % DEPTH);
+      for (unsigned spin = 0; __hip_atomic_load(full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)(k + 1);
+           ++spin) {
+        if (spin > SPIN) {
+          give_up(a.err);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
-    wait_slot(std::min(DEPTH - 1, nslot - 1 - k));
+    if (c == 0 && (k == 0 || k == 1 || k == 9 || k == 13)) stamp(a, 16 + (k == 0 ? 0 : (k == 1 ? 1 : (k == 9 ? 2 : 3))));
     u32x4_t wv[8];
     const u32x4_t* rp = reinterpret_cast<const u32x4_t*>(smem + L_RING + ((size_t)c * DEPTH + k % DEPTH) * SLOT) + lane;
 #pragma unroll
     for (int j = 0; j < 8; ++j) wv[j] = rp[j * 64];
-    if (k + DEPTH < nslot) issue_slot(slot_src<NEXT>(a, k + DEPTH, b, c), ring + ((k + DEPTH) % DEPTH) * SLOT, lane);
-    const bool second = k >= 9 && k <= 12 && ((k - 9) & 1);  // second half of an fc2 segment: the chain continues
-    const int base = second ? 8 : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) lds_st(smem, C_FREE + c * DEPTH + k % DEPTH, (unsigned)(k + 1));
     if (!second) acc0 = acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bf16x8_t w = __builtin_bit_cast(bf16x8_t, wv[j]);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xa0[base + j]), w, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, xa1[base + j]), w, acc1, 0, 0, 0);
+      const uint4 x0 = *reinterpret_cast<const uint4*>(xb + j * 64);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(xb + j * 64 + 32);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), w, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), w, acc1, 0, 0, 0);
     }
-    if (k >= 9 && k <= 12 && !second) continue;
+    if (f2 && !second) continue;
     float v[MAXR];
 #pragma unroll
     for (int q = 0; q < MAXR; ++q) v[q] = acc0[q] + ror8(acc1[q]);  // gemv_body step 5
@@ -222,7 +328,8 @@ __device__ __forceinline__ void consumer(const LArgs& a, char* smem, int b, int 
 #pragma unroll
         for (int q = 0; q < MAXR; ++q) redf[(((k - 1) * NCW + c) * 8 + col) * MAXR + q] = v[q];
       lds_arrive(cnt(smem, C_F1 + k - 1), lane);
-    } else if (k <= 12) {
+      if (k == 8) stamp(a, 20 + c);
+    } else if (f2) {
       const int g = 8 * m + 2 * c + ((k - 9) >> 1);
       uint64_t* gp = a.gran + Gran(a.M).gp;
       if (mine)
@@ -231,6 +338,7 @@ __device__ __forceinline__ void consumer(const LArgs& a, char* smem, int b, int 
           if (q < a.M)
             st_wt64(gp + (((size_t)g * 8 + s) * a.M + q) * 8 + col,
                     (uint64_t)__float_as_uint(v[q]) | ((uint64_t)tag[q] << 32));
+      if (k == 12) stamp(a, 24 + c);
     } else {
       if (mine)
 #pragma unroll
@@ -238,6 +346,14 @@ __device__ __forceinline__ void consumer(const LArgs& a, char* smem, int b, int 
       lds_arrive(cnt(smem, C_N + k - 13), lane);
     }
   }
+}
+
+// a service wave polls: the block's loader keeps `a.thin` slots in flight meanwhile
+__device__ __forceinline__ void thin_on(char* smem, int lane) {
+  if (lane == 0) __hip_atomic_fetch_add(cnt(smem, C_THIN), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void thin_off(char* smem, int lane) {
+  if (lane == 0) __hip_atomic_fetch_sub(cnt(smem, C_THIN), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // service-wave barrier (the consumers do not take part); n counts this wave's barriers, the same count in
@@ -334,7 +450,10 @@ __device__ __forceinline__ void attention(const LArgs& a, char* smem, int b, int
         for (int g = 0; g < XG; ++g) sc[g][key - CH * c] = sv[g] * a.scale;
       }
     }
+    if (sw == 0) stamp(a, 10);
     svc_sync(smem, nsync, lane, err);
+    if (sw == 0 && lane == 0) lds_st(smem, C_HOLD, 0u);  // the chunk's K / V have landed: weights may stream
+    if (sw == 0) stamp(a, 11);
     // (3) wave 0: the chunk maxima out as granules, then M_j of the chunk's block from the maxima of
     // chunks 0 .. dep - 1 (max is exact in any order)
     if (sw == 0) {
@@ -368,6 +487,7 @@ __device__ __forceinline__ void attention(const LArgs& a, char* smem, int b, int
       v = fmaxf(v, __shfl_xor(v, 32));
       if (lane < XG) mj[lane] = v;
     }
+    if (sw == 0) stamp(a, 12);
     svc_sync(smem, nsync, lane, err);
     // (4) wave g: e = exp(s - M_j), l (lane L: keys L, L + 64, then wave_sum), P = bf16(e)
     {
@@ -416,6 +536,7 @@ __device__ __forceinline__ void attention(const LArgs& a, char* smem, int b, int
         }
     }
     svc_sync(smem, nsync, lane, err);
+    if (sw == 0) stamp(a, 13);
     // (6) the chunk's P.V (groups summed in group order) out as granules, two (head, dim) per thread
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -429,10 +550,12 @@ __device__ __forceinline__ void attention(const LArgs& a, char* smem, int b, int
   } else {
     svc_sync(smem, nsync, lane, err);  // the chunk-live blocks' last barrier count is theirs alone: harmless
   }
-  // (7) dims 4 c .. 4 c + 3 of the unit's output: the block recursion of zmi_attn_merge.h over every chunk's
-  // partial, l and M_j, one (head, dim) per lane of wave 0; out as {pair, tag} granules of the attention rows
-  if (sw == 0) {
-    const int g = (lane >> 2) & 3, d = MDIM * c + (lane & 3);
+  // (7) chunk blocks 0..7: dims 16 c .. 16 c + 15 of the unit's output, the block recursion of zmi_attn_merge.h
+  // over every chunk's partial, l and M_j, one (head, dim) per lane of wave 0; out as {pair, tag} granules of
+  // the attention rows
+  if (sw == 0 && c < NMRG) {
+    thin_on(smem, lane);
+    const int g = lane >> 4, d = MDIM * c + (lane & 15);
     float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
     for (int k0 = 0; k0 < nc; k0 += 8) {
       uint64_t ov[8], lv[8], mv[2];
@@ -493,15 +616,17 @@ __device__ __forceinline__ void attention(const LArgs& a, char* smem, int b, int
         }
       }
     }
+    stamp(a, 14);
     const float rl = 1.0f / l;
     const uint32_t ov = f2bf(acc * rl);
     const uint32_t nb = (uint32_t)__shfl_down((int)ov, 1);
     const int col = (kh * XG + g) * HD + d;
-    if (lane < XG * MDIM) {
+    {
       if ((lane & 1) == 0)
         st_wt64(a.gran + G.ga + (size_t)r * (DM / 2) + (col >> 1), (uint64_t)(ov | (nb << 16)) | tag64);
       if (a.attn_out) a.attn_out[(size_t)r * DM + col] = (bf16_t)ov;
     }
+    thin_off(smem, lane);
   }
 }
 
@@ -528,12 +653,27 @@ __device__ __forceinline__ void service(const LArgs& a, char* smem, int b, int s
   if (own && lane < 8) xres = a.x[(size_t)sw * DM + 8 * b + lane];
   unsigned nsync = 0;
   attention(a, smem, b, sw, lane, nsync, a.err);
+  if (sw == 0 && lane == 0) lds_st(smem, C_PFGO, 1u);
+  // the norm2 / next-norm parameters into registers now (their loads are far from the critical path here)
+  uint4 ln2g[4], ln2b[4], lnng[4], lnnb[4];
+  if (own) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ln2g[q] = *reinterpret_cast<const uint4*>(a.ln2_w + q * 512 + lane * 8);
+      ln2b[q] = *reinterpret_cast<const uint4*>(a.ln2_b + q * 512 + lane * 8);
+      lnng[q] = *reinterpret_cast<const uint4*>(a.lnn_w + q * 512 + lane * 8);
+      lnnb[q] = *reinterpret_cast<const uint4*>(a.lnn_b + q * 512 + lane * 8);
+    }
+  }
+  thin_on(smem, lane);
   if (sw == 0) stamp(a, 1);
+  stamp(a, 28 + sw);
   svc_sync(smem, nsync, lane, a.err);  // the attention scratch (BUFA / BUFB) is free
   // (1) the attention rows -> BUFA (out_proj's activations)
   if (rlive)
     gather<512 / 64>(gr + G.ga + (size_t)rr * (DM / 2) + 512 * half, reinterpret_cast<uint32_t*>(bufA + rr * XROW) + 512 * half,
                      rtag, lane, a.err);
+  thin_off(smem, lane);
   if (sw == 0) stamp(a, 2);
   lds_arrive(cnt(smem, C_READY), lane);
   // (2) out_proj epilogue (EPI_RESIDUAL) of row sw: x' = bf16(x + bf16(segment sums in order)), out as granules
@@ -553,12 +693,15 @@ __device__ __forceinline__ void service(const LArgs& a, char* smem, int b, int s
   }
   if (sw == 0) stamp(a, 3);
   // (3) x' of every block -> BUFB, then norm2 in place (fc1's activations)
+  if (sw == 0 && lane == 0) lds_st(smem, C_PFSTOP, 1u);
+  thin_on(smem, lane);
   if (rlive)
     gather<512 / 64>(gr + G.gx + (size_t)rr * (DM / 2) + 512 * half, reinterpret_cast<uint32_t*>(bufB + rr * XROW) + 512 * half,
                      rtag, lane, a.err);
+  thin_off(smem, lane);
   if (sw == 0) stamp(a, 4);
   svc_sync(smem, nsync, lane, a.err);
-  if (own) ln_row(bufB + sw * XROW, a.ln2_w, a.ln2_b, a.eps, lane);
+  if (own) ln_row_r(bufB + sw * XROW, ln2g, ln2b, a.eps, lane);
   lds_arrive(cnt(smem, C_READY), lane);
   // (4) fc1 epilogues (EPI_SWIGLU, M8 packing: columns 0..3 values, 4..7 gates): groups sw and sw + 4, lane =
   // (row, column), out as h granules
@@ -589,12 +732,16 @@ __device__ __forceinline__ void service(const LArgs& a, char* smem, int b, int s
     }
   }
   if (sw == 0) stamp(a, 5);
+  stamp(a, 32 + sw);
   // (5) h segment s (fc2's activations for this block's K segment), produced by team s -> BUFA
+  thin_on(smem, lane);
   if (rlive)
     gather<256 / 64>(gr + G.gh + (size_t)rr * (FF / 2) + 512 * s + 256 * half,
                      reinterpret_cast<uint32_t*>(bufA + rr * XROW) + 256 * half, rtag, lane, a.err);
+  thin_off(smem, lane);
   if (sw == 0) stamp(a, 6);
   lds_arrive(cnt(smem, C_READY), lane);
+  thin_on(smem, lane);
   // (6) fc2 group b of row sw: the 8 segment sums (blocks 8 (b >> 3) + s') in segment order + the residual x'
   if (own) {
     const int sp = lane >> 3, cc = lane & 7;
@@ -614,9 +761,10 @@ __device__ __forceinline__ void service(const LArgs& a, char* smem, int b, int s
   if (rlive)
     gather<512 / 64>(gr + G.gy + (size_t)rr * (DM / 2) + 512 * half, reinterpret_cast<uint32_t*>(bufB + rr * XROW) + 512 * half,
                      rtag, lane, a.err);
+  thin_off(smem, lane);
   if (sw == 0) stamp(a, 8);
   svc_sync(smem, nsync, lane, a.err);
-  if (own) ln_row(bufB + sw * XROW, a.lnn_w, a.lnn_b, a.eps, lane);
+  if (own) ln_row_r(bufB + sw * XROW, lnng, lnnb, a.eps, lane);
   lds_arrive(cnt(smem, C_READY), lane);
   // (8) the next op's epilogues: item i (column group b + 256 i) on wave i % 4
   const int nn = n_next<NEXT>(b);
@@ -669,6 +817,7 @@ __device__ __forceinline__ void service(const LArgs& a, char* smem, int b, int s
     }
   }
   if (sw == 0) stamp(a, 9);
+  stamp(a, 36 + sw);
 }
 
 template <int NEXT>
@@ -676,15 +825,26 @@ __global__ __launch_bounds__(NT) void layer_engine_kernel(const LArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tid < 16) *cnt(smem, tid) = 0u;
   unsigned tag[MAXR];
 #pragma unroll
   for (int r = 0; r < MAXR; ++r) tag[r] = r < a.M ? (unsigned)(a.row_pos[r] + 1) : 0u;
+  if (tid < C_WORDS) {
+    unsigned v = 0u;
+    const int r = (b & 7) >> 2, pos = r < a.M ? a.row_pos[r] : -1;
+    const bool live = pos >= 0 && (b >> 3) <= pos / CH, merge = pos >= 0 && (b >> 3) < NMRG;
+    if (tid == C_HOLD && a.hold) v = live ? 1u : 0u;  // this block loads a live attention chunk's K / V first
+    if (tid == C_PFGO) v = (live || merge) ? 0u : 1u;  // attention blocks prefetch once their chunk is done
+    *cnt(smem, tid) = v;
+  }
   __syncthreads();
-  if (wave < NCW)
-    consumer<NEXT>(a, smem, b, wave, lane, tag);
+  if (wave < NLW)
+    loader<NEXT>(a, smem, b, wave, lane);
+  else if (wave < NLW + NCW)
+    consumer<NEXT>(a, smem, b, wave - NLW, lane, tag);
+  else if (wave < NLW + NCW + NSW)
+    service<NEXT>(a, smem, b, wave - NLW - NCW, lane, tag);
   else
-    service<NEXT>(a, smem, b, wave - NCW, lane, tag);
+    prefetcher<NEXT>(a, smem, b, lane);
 }
 
 }  // namespace
@@ -732,8 +892,11 @@ extern "C" int zmi_layer_engine(const ZmiLayerEngineArgs* args, void* stream) {
   a.gran = (uint64_t*)e.gran;
   a.err = e.err;
   a.diag = (unsigned long long*)e.diag;
-  a.start = zmi_option(ZMI_OPT_ENG_START);
-  a.spare = zmi_option(ZMI_OPT_ENG_SPARE);
+  a.fly = std::max(1, std::min(MAXFLY, zmi_option(ZMI_OPT_ENG_FLY)));
+  a.thin = std::max(1, std::min(a.fly, zmi_option(ZMI_OPT_ENG_THIN)));
+  a.hold = zmi_option(ZMI_OPT_ENG_HOLD);
+  a.pf = zmi_option(ZMI_OPT_ENG_PF);
+  a.delay = zmi_option(ZMI_OPT_ENG_DELAY);
   hipStream_t s = (hipStream_t)stream;
   if (e.next == 0) {
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&layer_engine_kernel<NEXT_QKV>),

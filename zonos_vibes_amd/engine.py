@@ -146,12 +146,16 @@ class HipEngine:
         # write the next LayerNorm; identical bits); 0 = never. out_proj split-K: C5-shaped 16-row step 1.732 vs
         # 1.741 ms, C3 sample 151.3 vs 149.5x (profiles/r03_splitk_oproj2_ab.jsonl)
         # out_proj + norm2 + fc1 + fc2 as ONE persistent launch (zmi_ffn_engine: 256 workgroups, one per CU, LDS-DMA
-        # weight rings running ahead of the in-launch hand-offs) for <= 2 rows at the v0.1 dims; identical bits
-        self.ffn_engine = True
+        # weight rings running ahead of the in-launch hand-offs) for <= 2 rows at the v0.1 dims; identical bits.
+        # Off: 28.2 us per layer against 25.5 for the three launches (tools/ffn_engine_bench.py)
+        self.ffn_engine = False
         # the whole decode layer as ONE persistent launch (zmi_layer_engine: attention, out_proj, fc1, fc2 and the
         # next layer's QKV / the heads, 256 workgroups, LDS-DMA weight rings) for <= 2 rows at the v0.1 dims and
-        # positions <= zmi_layer_engine_max_pos(); identical bits (the "engine" form)
-        self.layer_engine = True
+        # positions <= zmi_layer_engine_max_pos(); identical bits (the "engine" form). Off: the C2 step takes
+        # 1138-1167 us with it against 1011-1018 us with the launch plan on the same box (tools/step_ab.py,
+        # profiles/r04_engine_*): each in-launch all-gather costs ~3 us against ~1.5 us for a kernel boundary
+        # 
+        self.layer_engine = False
         self.splitk_rows = 16
         self.splitk_o_rows = 16
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
