@@ -104,7 +104,9 @@ def time_dominant_kernel(model, cond, reps: int = 3):
     return tot / (reps * len(items)), bytes_launch, name
 
 
-DOMINANT_KERNEL = "layer_engine_kernel<0>"
+# the committed FETCH_SIZE pass of each dominant-kernel candidate (tools/prof_round.sh)
+PMC_FILES = {"layer_engine_kernel<0>": "r04_pmc_engine_fetch.json",
+             "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": "r04_pmc_fc1_fetch.json"}
 
 
 def _time_fused(e, items, gran, run, reps: int) -> float:
@@ -126,22 +128,20 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
     return tot / (reps * len(items))
 
 
-PMC_FILE = "r04_pmc_engine_fetch.json"
-
-
-def pmc_traffic():
+def pmc_traffic(kernel: str):
     """HBM bytes per launch of the dominant kernel from the committed FETCH_SIZE pass of THIS kernel
     (tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950
     correction; a counter pass serialises dispatches, so it is not repeated inside the timed run). None
     when the profile is absent or measured another kernel."""
-    path = os.path.join(REPO, "profiles", PMC_FILE)
-    if not os.path.exists(path):
-        return None
+    name = PMC_FILES.get(kernel)
+    path = os.path.join(REPO, "profiles", name) if name else None
+    if not path or not os.path.exists(path):
+        return None, None
     with open(path) as f:
         d = json.load(f)
-    if not d.get("kernels") or any(DOMINANT_KERNEL not in k for k in d["kernels"]):
-        return None
-    return int(d["FETCH_SIZE_bytes_per_launch"])
+    if not d.get("kernels") or any(kernel not in k for k in d["kernels"]):
+        return None, None
+    return int(d["FETCH_SIZE_bytes_per_launch"]), f"profiles/{name}"
 
 
 def time_decode_step(model, cond, steps: int = 64):
@@ -828,6 +828,7 @@ def main():
     out = None
     if rank == 0:
         achieved = bl / (us * 1e-6) / 1e9
+        traffic, traffic_src = pmc_traffic(dom_name)
         out = {
             "metric": "real-time factor (44kHz audio s/compute s) + DAC tokens/s/GPU, Zonos-transformer",
             "value": round(rtf, 3), "unit": "x realtime (audio s / wall s, all GPUs)",
@@ -848,8 +849,8 @@ def main():
                                                 "+ the layer's K / V per launch)" if "engine" in dom_name else
                                                 " (fc1: LayerNorm prologue + packed SwiGLU epilogue, 67.1 MB)"),
                          "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": pmc_traffic(),
-                         "traffic_source": f"profiles/{PMC_FILE} (rocprofv3 FETCH_SIZE x2, bytes/launch)",
+                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
+                         "traffic_source": f"{traffic_src} (rocprofv3 FETCH_SIZE x2, bytes/launch)",
                          "avg_us": round(us, 2), "bytes_per_launch": bl},
             "codes_sha256_16": codes_sha,
             "c2_step_kernels": ktab,

@@ -1,0 +1,140 @@
+"""Full-depth parity at the positions the headline config and longer batch-1 utterances reach: Zonos-v0.1-
+transformer dims (26 layers), C2 conditioning (Lc = 160), synthetic weights -- the HIP path against the REFERENCE's
+own teacher-forced outputs along its 1,125-frame greedy trajectory (tests/golden/full_model_long.safetensors,
+make_golden_full_long.py; reference zonos/model.py:240-307, zonos/backbone/_torch.py:99-152).
+
+The decode steps run at positions 162 .. 1,294 and cross every form switch of the launch plan (the chunk-split
+fused attention to position 1,023, the score-exchange form to 1,279, the separate QKV + chunked attention beyond)
+and the softmax blocks of 512 keys. Criteria (the reference's own thread-count noise at these positions is the
+yardstick, fixture metadata `self_noise`):
+  * every teacher-forced greedy decision whose reference margin exceeds twice that noise is identical;
+  * CFG'd logits of the recorded windows (positions 588-596, 1,018-1,028, 1,278-1,292): mean error within 1.5x
+    the noise mean, max within 2x the noise max (bf16 ulps of each decision's top score);
+  * free-running generate(): the first divergence from the reference trajectory, if any, is at a decision the
+    reference leaves undetermined.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ulp(x: torch.Tensor) -> torch.Tensor:
+    return torch.ldexp(torch.ones_like(x), torch.frexp(x.abs().clamp_min(1e-30))[1] - 8)
+
+
+def _cfg_logits(rows):
+    c, u = rows[0].float().cpu(), rows[1].float().cpu()
+    lg = u + (c - u) * 2.0
+    lg[..., 1025:] = -torch.inf
+    return lg
+
+
+@pytest.fixture(scope="module")
+def long_fix():
+    from zonos_vibes_amd import synthetic as syn
+    from zonos_vibes_amd.config import ZonosConfig
+    from zonos_vibes_amd.model import Zonos
+    t, meta = load_golden("full_model_long")
+    cfg = ZonosConfig.from_dict(meta["cfg"])
+    lc, n = meta["lc"], meta["n"]
+    cond = torch.from_numpy(syn.synthetic_conditioning_np(meta["cond_seed"], 2, lc, cfg.backbone.d_model)
+                            .view(np.int16).copy()).view(torch.bfloat16)
+    model = Zonos.synthetic(cfg, DEV, seed=meta["weights_seed"], zero_eos=meta["zero_eos"],
+                            max_seqlen=lc + n + 24, max_prefill=lc + 8)
+    yield model, t, meta, cond
+    del model
+    torch.cuda.empty_cache()
+
+
+def test_full_depth_long_teacher_forced(long_fix):
+    from oracle.zonos_cpu import apply_delay_pattern, repetition_penalty
+    from zonos_vibes_amd.engine import SamplingParams
+    model, t, meta, cond = long_fix
+    e = model.engine
+    n, lc = meta["n"], meta["lc"]
+    noise = meta["self_noise"]
+    e.prefill(0, cond.to(DEV), None, n, SamplingParams(temperature=0.0))
+    e.stream.synchronize()
+    delayed = apply_delay_pattern(t["codes"], 1025)[0]
+    with torch.cuda.stream(e.stream):
+        e.delayed[0, :, : delayed.shape[-1]] = delayed.to(DEV, torch.int32)
+        e.refresh_inputs()
+    bias = torch.zeros(9, 1026)
+    bias[1:, 1024] = -torch.inf
+    win = set(int(s) for s in t["win_steps"])
+    scores = [_cfg_logits(e.logits_pre)]
+    win_logits, forms = [], set()
+    for s in range(n + 8):
+        o = int(e.st["offset"][0].item())
+        forms.add(e._segments(1, 1)[0][1])
+        e.step(1, slots=1)  # graph replay, the form the position calls for
+        e.stream.synchronize()
+        lg = _cfg_logits(e.logits[0:2])
+        if s in win:
+            win_logits.append(lg)
+        scores.append(repetition_penalty((lg + bias).unsqueeze(0), delayed[None, :, : o + 1], 3.0, 2)[0])
+    e.check_errors()
+    e.release(0)
+    # window logits against the reference's
+    errs = []
+    for got, r in zip(win_logits, t["win_logits"]):
+        fin = torch.isfinite(r)
+        assert torch.equal(fin, torch.isfinite(got))
+        top = r.masked_fill(~fin, -torch.inf).max(-1).values
+        errs.append((got - r).masked_fill(~fin, 0).abs().max(-1).values / _ulp(top))
+    errs = torch.cat(errs)
+    # every decision along the reference trajectory (decision i writes frame i + 1 into the codebooks still
+    # unknown there, model.py:258-260,296-297)
+    floor = 2 * noise["max_ulps"]
+    det = t["margin"] > floor * _ulp(t["top"])
+    got_arg = torch.stack([sc.argmax(-1) for sc in scores])
+    init = apply_delay_pattern(torch.full((1, 9, n), -1), 1025)[0]
+    agree = torch.ones_like(det)
+    used = torch.zeros_like(det)
+    for i in range(min(got_arg.shape[0], init.shape[1] - 1)):
+        unk = (init[:, i + 1] == -1).nonzero().flatten().tolist()
+        for m, k in enumerate(unk):
+            used[i, m] = True
+            agree[i, m] = bool(got_arg[i, m] == delayed[k, i + 1])
+    det = det & used
+    bad = (det & ~agree).nonzero().tolist()
+    stats = dict(positions=[lc + 1, lc + n + 8], forms=sorted(forms), window_steps=len(win_logits),
+                 mean_err_ulps=float(errs.mean()), max_err_ulps=float(errs.max()), ref_self_noise=noise,
+                 within_thread_noise_frac=float((errs <= noise["max_ulps"]).float().mean()),
+                 decisions=int(used.sum()), agree=int((agree & used).sum()), determined=int(det.sum()),
+                 determined_disagreements=len(bad), first_bad=bad[:5])
+    if os.path.isdir("gpurun_out"):
+        json.dump(stats, open("gpurun_out/full_parity_long.json", "w"), indent=1)
+    assert stats["determined_disagreements"] == 0, stats
+    assert errs.mean() <= 1.5 * noise["mean_ulps"], stats
+    assert errs.max() <= 2 * noise["max_ulps"], stats
+
+
+def test_full_depth_long_greedy_trajectory(long_fix):
+    from oracle.zonos_cpu import apply_delay_pattern
+    model, t, meta, cond = long_fix
+    n = meta["n"]
+    out = model.generate(cond.to(DEV), max_new_tokens=n, sampling_params=dict(temperature=0.0), progress_bar=False,
+                         chunk=128)
+    got = apply_delay_pattern(out.cpu(), 1025)[0]
+    ref = apply_delay_pattern(t["codes"], 1025)[0]
+    diff = (got != ref)
+    info = dict(identical=not bool(diff.any()))
+    if diff.any():
+        f = int(diff.any(0).nonzero()[0])
+        k = int(diff[:, f].nonzero()[0])
+        margin, top = float(t["margin"][f - 1, k]), float(t["top"][f - 1, k])
+        floor = 2 * meta["self_noise"]["max_ulps"] * float(_ulp(torch.tensor(top)))
+        info.update(first_diverging_frame=f, position=meta["lc"] + f, codebook=k, ref_margin=margin, floor=floor)
+    if os.path.isdir("gpurun_out"):
+        json.dump(info, open("gpurun_out/full_trajectory_long.json", "w"), indent=1)
+    if diff.any():
+        assert info["ref_margin"] <= info["floor"], f"divergence at a decision the reference determines: {info}"
