@@ -79,7 +79,7 @@ def time_dominant_kernel(model, cond, reps: int = 3):
 
         def run():
             for it in items:
-                _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
+                _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
         bytes_launch, name = engine_bytes(e, pos), "layer_engine_kernel<0>"
     else:
         items = [item for kind, item in e._plan(2, form) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
@@ -92,7 +92,8 @@ def time_dominant_kernel(model, cond, reps: int = 3):
         bytes_launch, name = 2 * F * d * 2 + 2 * d * 2 + 2 * d * 2 + 2 * F * 2, "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"
     with torch.cuda.stream(e.stream):
         for r in range(reps + 1):
-            e.lay_gran.zero_()
+            if form == "engine":
+                e.lay_gran.zero_()
             st.record(e.stream)
             run()
             en.record(e.stream)
@@ -282,10 +283,10 @@ def _engine_kernel_table(e, plan, pos: int, reps: int) -> dict:
     kinds = {"qkv layer 0 (gemv: LN + QKV + RoPE + KV write)": (lambda it: e._run_gemv(it), qkv0,
                                                                   (e.H + 2 * e.Hkv) * e.hd * e.d * 2),
              "layer_engine<0> (attention + out_proj + fc1 + fc2 + next LN/QKV)":
-                 (lambda it: _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 0],
+                 (lambda it: _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 0],
                   engine_bytes(e, pos, 0)),
              "layer_engine<1> (attention + out_proj + fc1 + fc2 + norm_f + heads)":
-                 (lambda it: _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 1],
+                 (lambda it: _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 1],
                   engine_bytes(e, pos, 1))}
     with torch.cuda.stream(e.stream):
         for name, (run, items, nbytes) in kinds.items():

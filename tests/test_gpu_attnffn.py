@@ -11,7 +11,10 @@ import torch
 
 from tests.test_gpu_kernels import DEV, _lib, pack, rnd, stream_ptr
 
-pytestmark = pytest.mark.gpu
+from zonos_vibes_amd import _lib as _zl  # noqa: E402
+
+# a diagnostic form (include/zonos_diag.h): tested when libzonos_diag.so is built (`build --diag`)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _zl.diag_available(), reason="libzonos_diag.so not built")]
 
 D, F, H, HKV, HD = 2048, 8192, 16, 4, 128
 
@@ -38,7 +41,7 @@ def test_attn_ffn_block_bit_identical_to_separate_launches(positions):
     if torch.cuda.get_device_properties(0).multi_processor_count < 256:
         pytest.skip("zmi_attn_ffn_block needs 256 CUs")
     M, smax = len(positions), 1032
-    assert max(positions) <= L.lib().zmi_attn_ffn_max_pos()
+    assert max(positions) <= L.diag().zmi_attn_ffn_max_pos()
     q = rnd(M, H * HD, scale=1.0, seed=80)
     kc = rnd(M, HKV, smax, HD, seed=81)
     vt = rnd(M, HKV, HD, smax, seed=82)
@@ -71,15 +74,15 @@ def test_attn_ffn_block_bit_identical_to_separate_launches(positions):
     qa.row_pos, qa.k_cache, qa.v_cache = row_pos.data_ptr(), kc.data_ptr(), vt.data_ptr()
     qa.smax, qa.hq, qa.hkv, qa.hd = smax, H, HKV, HD
     xg = _stale(L.lib().zmi_attn_block_gran_words(M, HKV))
-    og = _stale(L.lib().zmi_attn_ffn_gran_words(M))
-    rg = _stale(L.lib().zmi_attn_ffn_gran_words(M))
+    og = _stale(L.diag().zmi_attn_ffn_gran_words(M))
+    rg = _stale(L.diag().zmi_attn_ffn_gran_words(M))
     err = torch.zeros(4, dtype=torch.int32, device=DEV)
     for rep in range(3):
         attn_f = attn0.clone()
         xf, hf = x0.clone(), torch.zeros(M, F, dtype=torch.bfloat16, device=DEV)
         a = _gemv_args(Po, attn_f, M, D, D, xf, D, row_pos=row_pos)
         b = _gemv_args(Pf, xf, M, 2 * F, D, hf, F, ln=ln)
-        L.check(L.lib().zmi_attn_ffn_block(ctypes.byref(qa), ctypes.byref(a), ctypes.byref(b), xg.data_ptr(),
+        L.check(L.diag().zmi_attn_ffn_block(ctypes.byref(qa), ctypes.byref(a), ctypes.byref(b), xg.data_ptr(),
                                            og.data_ptr(), rg.data_ptr(), err.data_ptr(), attn_f.data_ptr(), H * HD,
                                            stream_ptr()), "attn_ffn_block")
         torch.cuda.synchronize()

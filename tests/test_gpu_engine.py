@@ -8,7 +8,10 @@ import torch
 
 from tests.test_gpu_kernels import DEV, _lib, pack, rnd, stream_ptr
 
-pytestmark = pytest.mark.gpu
+from zonos_vibes_amd import _lib as _zl  # noqa: E402
+
+# a diagnostic form (include/zonos_diag.h): tested when libzonos_diag.so is built (`build --diag`)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _zl.diag_available(), reason="libzonos_diag.so not built")]
 
 D, F = 2048, 8192
 
@@ -38,7 +41,7 @@ def _engine(L, Po, Pf, P2, ln, attn, x, h, row_pos, gran, err, diag=None):
     e.ld_attn, e.ldx, e.ldh = attn.shape[1], x.shape[1], F
     e.row_pos, e.gran, e.err = row_pos.data_ptr(), gran.data_ptr(), err.data_ptr()
     e.diag = diag.data_ptr() if diag is not None else None
-    L.check(L.lib().zmi_ffn_engine(ctypes.byref(e), stream_ptr()), "ffn_engine")
+    L.check(L.diag().zmi_ffn_engine(ctypes.byref(e), stream_ptr()), "ffn_engine")
 
 
 @pytest.mark.parametrize("positions", [(591, 591), (0,), (1023, 1023), (5000, 5000)])
@@ -57,7 +60,7 @@ def test_ffn_engine_bit_identical_to_separate_launches(positions):
     _gemv(L, Pf, xs, M, 2 * F, D, hs, F, L.EPI_SWIGLU, ln=ln)
     _gemv(L, P2, hs, M, D, F, xs, D, L.EPI_RESIDUAL)
     # engine: three launches at the same position over granules holding stale tags, then at the next position
-    gran = torch.randint(0, 1 << 30, (L.lib().zmi_ffn_engine_gran_words(M),), device=DEV, dtype=torch.int64)
+    gran = torch.randint(0, 1 << 30, (L.diag().zmi_ffn_engine_gran_words(M),), device=DEV, dtype=torch.int64)
     gran |= torch.randint(1 << 20, 1 << 30, gran.shape, device=DEV) << 32
     err = torch.zeros(4, dtype=torch.int32, device=DEV)
     for rep in range(3):
@@ -89,7 +92,7 @@ def test_ffn_engine_layer_chain():
         _gemv(L, Po, at, M, D, D, xs, D, L.EPI_RESIDUAL)
         _gemv(L, Pf, xs, M, 2 * F, D, hs, F, L.EPI_SWIGLU, ln=ln)
         _gemv(L, P2, hs, M, D, F, xs, D, L.EPI_RESIDUAL)
-    words = L.lib().zmi_ffn_engine_gran_words(M)
+    words = L.diag().zmi_ffn_engine_gran_words(M)
     gran = torch.zeros(NL, words, dtype=torch.int64, device=DEV)
     err = torch.zeros(4, dtype=torch.int32, device=DEV)
     xf = x0.clone()

@@ -9,7 +9,10 @@ import torch
 
 from tests.test_gpu_kernels import DEV, _lib, pack, rnd, stream_ptr
 
-pytestmark = pytest.mark.gpu
+from zonos_vibes_amd import _lib as _zl  # noqa: E402
+
+# a diagnostic form (include/zonos_diag.h): tested when libzonos_diag.so is built (`build --diag`)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _zl.diag_available(), reason="libzonos_diag.so not built")]
 
 D, F = 2048, 8192
 
@@ -47,7 +50,7 @@ def test_ffn_block_bit_identical_to_separate_launches(positions):
     b = _args(Pf, xs, M, 2 * F, D, hs, F, ln=ln)
     L.check(L.lib().zmi_gemv_launch(ctypes.byref(b), L.EPI_SWIGLU, stream_ptr()))
     # fused, three times at the same positions over granules holding stale tags
-    gran = torch.zeros(L.lib().zmi_ffn_block_gran_words(M), dtype=torch.int64, device=DEV)
+    gran = torch.zeros(L.diag().zmi_ffn_block_gran_words(M), dtype=torch.int64, device=DEV)
     gran.copy_(torch.randint(0, 1 << 30, gran.shape, device=DEV) |
                (torch.randint(1 << 20, 1 << 30, gran.shape, device=DEV) << 32))
     err = torch.zeros(4, dtype=torch.int32, device=DEV)
@@ -55,7 +58,7 @@ def test_ffn_block_bit_identical_to_separate_launches(positions):
         xf, hf = x0.clone(), torch.zeros(M, F, dtype=torch.bfloat16, device=DEV)
         a = _args(Po, attn, M, D, D, xf, D, row_pos=row_pos)
         b = _args(Pf, xf, M, 2 * F, D, hf, F, ln=ln)
-        L.check(L.lib().zmi_ffn_block(ctypes.byref(a), ctypes.byref(b), gran.data_ptr(), err.data_ptr(),
+        L.check(L.diag().zmi_ffn_block(ctypes.byref(a), ctypes.byref(b), gran.data_ptr(), err.data_ptr(),
                                       stream_ptr()), "ffn_block")
         torch.cuda.synchronize()
         assert int(err[0].item()) == 0, "a hand-off wait gave up"

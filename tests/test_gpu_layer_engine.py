@@ -7,7 +7,10 @@ import torch
 
 from zonos_vibes_amd.config import transformer_config
 
-pytestmark = pytest.mark.gpu
+from zonos_vibes_amd import _lib as _zl  # noqa: E402
+
+# a diagnostic form (include/zonos_diag.h): tested when libzonos_diag.so is built (`build --diag`)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not _zl.diag_available(), reason="libzonos_diag.so not built")]
 DEV = "cuda"
 
 

@@ -24,7 +24,7 @@ def main():
     attn = rnd(M, D, scale=1.0, seed=5)
     x0 = rnd(M, D, scale=2.0, seed=6)
     h = torch.zeros(M, F, dtype=torch.bfloat16, device=DEV)
-    gran = torch.zeros(NL, L.lib().zmi_ffn_engine_gran_words(M), dtype=torch.int64, device=DEV)
+    gran = torch.zeros(NL, L.diag().zmi_ffn_engine_gran_words(M), dtype=torch.int64, device=DEV)
     err = torch.zeros(4, dtype=torch.int32, device=DEV)
     pos = [10]
 

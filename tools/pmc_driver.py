@@ -69,7 +69,7 @@ def main(which: str, reps: int = 2):
             e.lay_gran.zero_()
             for kind, it in plan:
                 if kind == "layereng" and it.next == 0:
-                    _lib.check(e.lib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
+                    _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
         else:
             raise SystemExit(f"unknown driver {which}")
     e.stream.synchronize()

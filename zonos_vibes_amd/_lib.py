@@ -125,21 +125,10 @@ _SIGS = {
     "zmi_attn_block_max_pos": (c_int, [c_int]),
     "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
-    "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
-    "zmi_ffn_block_gran_words": (c_int64, [c_int]),
-    "zmi_ffn_engine": (c_int, [ctypes.POINTER(FfnEngineArgs), c_void_p]),
-    "zmi_ffn_engine_gran_words": (c_int64, [c_int]),
-    "zmi_layer_engine": (c_int, [ctypes.POINTER(LayerEngineArgs), c_void_p]),
-    "zmi_layer_engine_gran_words": (c_int64, [c_int]),
-    "zmi_layer_engine_max_pos": (c_int, []),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,
                                    c_void_p, c_int, c_void_p]),
-    "zmi_attn_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs),
-                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
-    "zmi_attn_ffn_gran_words": (c_int64, [c_int]),
-    "zmi_attn_ffn_max_pos": (c_int, []),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,
                                   ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
@@ -188,8 +177,26 @@ _SIGS = {
     "zmi_get_option": (c_int, [c_int]),
 }
 
+# libzonos_diag.so (include/zonos_diag.h): measured-slower decode forms, built by `build --diag`
+_DIAG_SIGS = {
+    "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
+    "zmi_ffn_block_gran_words": (c_int64, [c_int]),
+    "zmi_ffn_engine": (c_int, [ctypes.POINTER(FfnEngineArgs), c_void_p]),
+    "zmi_ffn_engine_gran_words": (c_int64, [c_int]),
+    "zmi_layer_engine": (c_int, [ctypes.POINTER(LayerEngineArgs), c_void_p]),
+    "zmi_layer_engine_gran_words": (c_int64, [c_int]),
+    "zmi_layer_engine_max_pos": (c_int, []),
+    "zmi_attn_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs),
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "zmi_attn_ffn_gran_words": (c_int64, [c_int]),
+    "zmi_attn_ffn_max_pos": (c_int, []),
+}
+
 EXPORTED = sorted(_SIGS)
+DIAG_EXPORTED = sorted(_DIAG_SIGS)
+DIAG_PATH = os.path.join(HERE, "libzonos_diag.so")
 _lib = None
+_diag = None
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -211,6 +218,27 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         _lib = load()
     return _lib
+
+
+def diag_available() -> bool:
+    return os.path.exists(DIAG_PATH)
+
+
+def diag() -> ctypes.CDLL:
+    """The diagnostic library (zonos_diag.h). It is not part of the product path: nothing on by default calls it."""
+    global _diag
+    if _diag is None:
+        lib()  # libzonos_hip.so first: the diagnostic library resolves its error / option state there
+        if not diag_available():
+            raise RuntimeError(f"{DIAG_PATH} is missing: these decode forms are diagnostics, built only by "
+                               "`python -m zonos_vibes_amd.build --diag`")
+        d = ctypes.CDLL(DIAG_PATH)
+        for name, (res, args) in _DIAG_SIGS.items():
+            fn = getattr(d, name)
+            fn.restype = res
+            fn.argtypes = args
+        _diag = d
+    return _diag
 
 
 def check(rc: int, what: str = "") -> None:

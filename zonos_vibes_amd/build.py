@@ -1,4 +1,10 @@
-"""Build libzonos_hip.so in-tree with hipcc for gfx950 (no JIT cache, travels with the repo)."""
+"""Build libzonos_hip.so in-tree with hipcc for gfx950 (no JIT cache, travels with the repo).
+
+    python -m zonos_vibes_amd.build [--force] [--diag]
+
+--diag also builds libzonos_diag.so (include/zonos_diag.h): the fused / persistent decode forms measured slower
+than the product plan, kept for their tests and timing tools, linked against libzonos_hip.so.
+"""
 from __future__ import annotations
 
 import os
@@ -10,11 +16,12 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libzonos_hip.so")
+DIAG_LIB = os.path.join(HERE, "libzonos_diag.so")
 SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + ["zmi_attn.hip", "zmi_attnblk.hip", "zmi_sample.hip",
                                                                         "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip",
-                                                                        "zmi_mamba.hip", "zmi_mambablk.hip", "zmi_ffnblk.hip",
-                                                                        "zmi_attnffn.hip", "zmi_gemm_splitk.hip", "zmi_engine.hip",
-           "zmi_layer.hip"]
+                                                                        "zmi_mamba.hip", "zmi_mambablk.hip",
+                                                                        "zmi_gemm_splitk.hip"]
+DIAG_SOURCES = ["zmi_ffnblk.hip", "zmi_attnffn.hip", "zmi_engine.hip", "zmi_layer.hip"]
 HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_attn_merge.h", "zmi_attn_ds.h", "zmi_mamba_step.h",
            "zmi_prefetch.h", "zmi_engine.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -29,14 +36,21 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
+def build(force: bool = False, verbose: bool = True, jobs: int = 8, diag: bool = False) -> str:
+    lib = _build(SOURCES, LIB, [], force, verbose, jobs)
+    if diag:
+        # resolves zmi_fail_msg / zmi_option / zmi_cu_count from libzonos_hip.so next to it
+        _build(DIAG_SOURCES, DIAG_LIB, [f"-L{HERE}", "-lzonos_hip", "-Wl,-rpath,$ORIGIN"], force, verbose, jobs)
+    return lib
+
+
+def _build(sources: list[str], lib: str, link: list[str], force: bool, verbose: bool, jobs: int) -> str:
     objdir = os.path.join(HERE, "build")
-    lib = LIB
     flags = FLAGS
     os.makedirs(objdir, exist_ok=True)
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "zonos_hip.h")]
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, h) for h in ("zonos_hip.h", "zonos_diag.h")]
     objs, procs = [], []
-    for src in SOURCES:
+    for src in sources:
         sp = os.path.join(CSRC, src)
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         objs.append(obj)
@@ -51,7 +65,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
         _wait(p)
     if force or _stale(lib, objs):
         tmp = lib + ".tmp"  # linked aside, then renamed: a reader never sees a half-written library
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", tmp]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, *link, "-o", tmp]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
@@ -70,4 +84,4 @@ def _wait(item):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, diag="--diag" in sys.argv)

@@ -30,6 +30,7 @@
 
 #include "zmi_common.h"
 #include "zmi_kernels.h"
+#include "zonos_diag.h"
 #include "zmi_gemv_impl.h"
 #include "zmi_engine.h"
 

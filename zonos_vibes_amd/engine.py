@@ -170,6 +170,24 @@ class HipEngine:
         self.n_kv = self._kv_layers()
         self._alloc()
 
+    @property
+    def dlib(self):
+        """libzonos_diag.so: the fused / persistent decode forms measured slower than this plan (ffn_block,
+        attn_ffn, ffn_engine, layer_engine; all off by default). Loaded on first use; never on the product path."""
+        return _lib.diag()
+
+    def _diag_alloc(self):
+        """Hand-off granule areas of the diagnostic forms, zeroed (as a new utterance needs them)."""
+        if self.eng_gran is not None:
+            return
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=self.dev)  # noqa: E731
+        with torch.cuda.stream(self.stream):
+            one = self.S == 1 and not self.hybrid
+            self.eng_gran = z(self.L if one else 0, max(self.dlib.zmi_ffn_engine_gran_words(2), 0))
+            self.lay_gran = z(self.L if one else 0, max(self.dlib.zmi_layer_engine_gran_words(2), 0))
+            self.ffn_gran = z(self.L, self.R, self.dlib.zmi_ffn_block_gran_words(1))
+            self.attn_gran = z(self.L, self.R, self.dlib.zmi_attn_ffn_gran_words(1))
+
     def _kv_layers(self) -> int:
         """Layers with a KV cache (every layer of the transformer)."""
         return self.L
@@ -201,16 +219,8 @@ class HipEngine:
             self.blk_gran = z(self.n_kv, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
             self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block,
             # [4] attn_ffn_block, [5] ffn_engine, [6] layer_engine
-            # zmi_ffn_engine hand-off granules (batch 1: rows 0 and 1), one area per layer
-            ew = self.lib.zmi_ffn_engine_gran_words(2)
-            self.eng_gran = z(self.L if S == 1 and not self.hybrid else 0, max(ew, 0), dt=torch.int64)
-            # zmi_layer_engine hand-off granules (batch 1), one area per layer
-            lw_ = self.lib.zmi_layer_engine_gran_words(2)
-            self.lay_gran = z(self.L if S == 1 and not self.hybrid else 0, max(lw_, 0), dt=torch.int64)
-            # zmi_ffn_block hand-off granules (the new residual rows), one area per layer
-            self.ffn_gran = z(self.L, R, self.lib.zmi_ffn_block_gran_words(1), dt=torch.int64)
-            # zmi_attn_ffn_block hand-off granules (the attention output rows), one area per layer
-            self.attn_gran = z(self.L, R, self.lib.zmi_attn_ffn_gran_words(1), dt=torch.int64)
+            # hand-off granules of the diagnostic forms (zonos_diag.h), allocated on first use (_diag_alloc)
+            self.eng_gran = self.lay_gran = self.ffn_gran = self.attn_gran = None
             # zmi_gemv_splitk's fp32 segment sums (fc2 over many rows: decode and prefill)
             self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
             self.samp_cnt = z(S, dt=torch.int32)
@@ -346,6 +356,7 @@ class HipEngine:
                 and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
 
     def _layer_engine_args(self, i: int, rows: int) -> _lib.LayerEngineArgs:
+        self._diag_alloc()
         w, L = self.w, self.L
         lw, last = w["layers"][i], i + 1 == L
         e = _lib.LayerEngineArgs()
@@ -366,6 +377,7 @@ class HipEngine:
         return e
 
     def _ffn_engine_args(self, lw, i: int, rows: int) -> _lib.FfnEngineArgs:
+        self._diag_alloc()
         e = _lib.FfnEngineArgs()
         e.w_out, e.w_fc1, e.w_fc2 = lw["out"].data_ptr(), lw["fc1"].data_ptr(), lw["fc2"].data_ptr()
         e.ln_w, e.ln_b, e.eps = lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), self.eps
@@ -385,7 +397,7 @@ class HipEngine:
         QKV and attention launches (any position)."""
         out = []
         if self._use_layer_engine(rows):
-            out.append(("engine", self.lib.zmi_layer_engine_max_pos()))
+            out.append(("engine", self.dlib.zmi_layer_engine_max_pos()))
         if self.attn_block and rows <= self.attn_block_rows and self.d == 2048 and self.H == 4 * self.Hkv:
             for f in self.attn_forms:
                 if f != "xs" or rows <= self.attn_xs_rows:
@@ -536,14 +548,16 @@ class HipEngine:
 
     def _run_attn_ffn(self, item):
         a, o, f, i = item
-        _lib.check(self.lib.zmi_attn_ffn_block(ctypes.byref(a), ctypes.byref(o), ctypes.byref(f),
+        self._diag_alloc()
+        _lib.check(self.dlib.zmi_attn_ffn_block(ctypes.byref(a), ctypes.byref(o), ctypes.byref(f),
                                                self.blk_gran[i].data_ptr(), self.attn_gran[i].data_ptr(),
                                                self.ffn_gran[i].data_ptr(), self.blk_err[4:].data_ptr(),
                                                self.attn.data_ptr(), self.H * self.hd, self.sptr), "attn_ffn_block")
 
     def _run_ffn_block(self, item):
         o, f, i = item
-        _lib.check(self.lib.zmi_ffn_block(ctypes.byref(o), ctypes.byref(f), self.ffn_gran[i].data_ptr(),
+        self._diag_alloc()
+        _lib.check(self.dlib.zmi_ffn_block(ctypes.byref(o), ctypes.byref(f), self.ffn_gran[i].data_ptr(),
                                           self.blk_err[3:].data_ptr(), self.sptr), "ffn_block")
 
     def check_errors(self):
@@ -624,9 +638,9 @@ class HipEngine:
             elif kind == "attnffn":
                 self._run_attn_ffn(item)
             elif kind == "layereng":
-                _lib.check(self.lib.zmi_layer_engine(ctypes.byref(item), self.sptr), "layer_engine")
+                _lib.check(self.dlib.zmi_layer_engine(ctypes.byref(item), self.sptr), "layer_engine")
             elif kind == "ffneng":
-                _lib.check(self.lib.zmi_ffn_engine(ctypes.byref(item), self.sptr), "ffn_engine")
+                _lib.check(self.dlib.zmi_ffn_engine(ctypes.byref(item), self.sptr), "ffn_engine")
             elif kind == "splitkln":
                 (a, epi), ln = item
                 _lib.check(self.lib.zmi_gemv_splitk_ln(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
@@ -768,11 +782,12 @@ class HipEngine:
     def _reset_granules(self, slot: int):
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
         self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
-        self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
-        self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
-        if slot == 0:
-            self.eng_gran.zero_()
-            self.lay_gran.zero_()
+        if self.eng_gran is not None:  # the diagnostic forms' areas, once allocated
+            self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
+            self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
+            if slot == 0:
+                self.eng_gran.zero_()
+                self.lay_gran.zero_()
 
     def _prefill_logits(self, s_len: int, off: int = 0):
         """Heads of the last position of the cond / uncond prefill rows (starting at row `off`) -> logits_pre
