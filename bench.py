@@ -145,17 +145,18 @@ def pmc_traffic(kernel: str):
     return int(d["FETCH_SIZE_bytes_per_launch"]), f"profiles/{name}"
 
 
-def time_decode_step(model, cond, steps: int = 64):
+def time_decode_step(model, cond, steps: int = 64, n_new: int = N_NEW, at: int | None = None):
     """Decode-step time of a LIVE utterance (both CFG rows active) around its mean position.
 
-    Prefills slot 0 with the bench conditioning, runs to position Lc + N/2 - steps/2, then times
-    `steps` graph replays on the engine stream with HIP events. Returns (us per step, mean position).
+    Prefills slot 0 with the bench conditioning (an n_new-frame utterance), runs to position Lc + at - steps/2
+    (at = n_new / 2 by default), then times `steps` graph replays on the engine stream with HIP events. Returns
+    (us per step, mean position).
     """
     from zonos_vibes_amd.engine import SamplingParams
     e = model.engine
     params = SamplingParams(temperature=0.0, cfg_scale=2.0)
-    s_len = e.prefill(0, cond, None, N_NEW, params)
-    lead = max(0, N_NEW // 2 - steps // 2)
+    s_len = e.prefill(0, cond, None, n_new, params)
+    lead = max(0, (n_new // 2 if at is None else at) - steps // 2)
     e.step(lead, slots=1)
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(e.stream):
@@ -451,6 +452,40 @@ def time_default_capacity(dev, n_new: int, ref_codes) -> dict:
            "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3), "utterance_ms": round(el * 1e3, 1),
            "decode_step_us": round(us, 1), "decode_step_pos": pos,
            "codes_equal_c2": bool(torch.equal(codes, ref_codes))}
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
+def time_long_utterance(dev, n_new: int = 86 * 30) -> dict:
+    """One batch-1 utterance at the reference's default generate(max_new_tokens=86 * 30) (model.py:223: 30 s of
+    audio, contexts to Lc + 2580 positions): wall-clock RTF of generate() + DAC decode, and the decode step at
+    positions across the utterance (HIP events, 64 steps each) with the attention form the plan picks there."""
+    from zonos_vibes_amd.model import Zonos
+    cfg = zonos_v01_transformer()
+    m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n_new + 9, max_prefill=LC + 1)
+    cond = cond_tensor(1, cfg.backbone.d_model, dev)
+
+    def one():
+        codes = m.generate(cond, max_new_tokens=n_new, sampling_params=dict(temperature=0.0), progress_bar=False,
+                           chunk=128)
+        return codes, m.autoencoder.decode(codes)
+
+    one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes, _ = one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    steps = {}
+    for at in (430, 1000, 1200, 1600, 2000, 2500):
+        us, pos = time_decode_step(m, cond, n_new=n_new, at=at)
+        m.engine.pos_hi[0] = pos
+        steps[str(pos)] = {"us": round(us, 1), "form": m.engine._segments(1, 1)[0][1]}
+    out = {"config": f"batch 1, Lc {LC}, {n_new} new frames (30 s: the reference default max_new_tokens), greedy, EOS "
+                     f"suppressed, + DAC decode", "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3),
+           "utterance_ms": round(el * 1e3, 1), "frames": int(codes.shape[-1]),
+           "decode_step_us_by_position": steps}
     del m
     torch.cuda.empty_cache()
     return out
@@ -817,6 +852,7 @@ def main():
     widened = time_widened_rows(model, dev)
     if rank == 0 and not args.no_default_cap:
         widened["default_capacity"] = time_default_capacity(dev, n_new, ref_codes)
+        widened["batch1_30s"] = time_long_utterance(dev)
     if rank == 0 and not args.no_hybrid:
         widened["hybrid_c4"] = time_hybrid(dev, n_new)
     if rank == 0 and not args.no_c5:

@@ -103,9 +103,11 @@ int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cac
                   const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                   int ldo, float* part_o, float* part_lm, void* work, void* stream);
 /* Same op with an explicit kernel choice: 0 = library choice (as zmi_attention), 1 = the chunked
- * kernel above (any length), 4 / 8 = the whole-query kernel with that many output-dim slices
- * per (query, kv head): every slice reads all of the query's keys and no workgroup waits on
- * another (max_pos < zmi_attention_max_keys_whole()). All variants return identical bits. */
+ * kernel above (any length, one launch), 2 = the chunked kernel as two launches (scores and maxima, then the
+ * rest: no workgroup waits on another), 3 = three launches (the merge as its own launch), 4 / 8 = the
+ * whole-query kernel with that many output-dim slices per (query, kv head): every slice reads all of the
+ * query's keys and no workgroup waits on another (max_pos < zmi_attention_max_keys_whole()). All variants
+ * return identical bits. */
 int zmi_attention_variant(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                           const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                           int ldo, float* part_o, float* part_lm, void* work, int variant, void* stream);
@@ -145,6 +147,14 @@ typedef struct ZmiPrefetch {
 } ZmiPrefetch;
 int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                       const ZmiPrefetch* prefetch, void* stream);
+/* zmi_attention_variant plus prefetch-only workgroups (variant 0 / 1: `prefetch->blocks` of them at the end
+ * of the grid) that read prefetch->ptr[0..1][0 .. bytes) once, so the next launches (out_proj, the head of
+ * fc1) find those weights in the Infinity Cache: they run on the CUs the chunks vacate, while the chunks
+ * exchange maxima and merge (HBM nearly idle). prefetch may be NULL. Results are zmi_attention_variant's. */
+int zmi_attention_pf(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
+                     const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out, int ldo,
+                     float* part_o, float* part_lm, void* work, int variant, const ZmiPrefetch* prefetch,
+                     void* stream);
 int64_t zmi_attention_work_bytes(int n_query, int hq, int hkv, int hd, int max_pos);
 int64_t zmi_attention_partial_floats(int n_query, int hq, int hkv, int hd, int max_pos);
 int zmi_attention_chunk(void);

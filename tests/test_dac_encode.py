@@ -82,6 +82,15 @@ def test_vq_kernel_on_reference_latents(gold, weights):
 
 @pytest.mark.gpu
 def test_hip_encode_matches_reference(gold, weights):
+    """HIP encoder (f16 MFMA convs, fp32 accumulation) + VQ against the reference's fp32 DacModel.encode.
+    The parity criterion is `bad`: in every frame whose codes differ, the FIRST differing codebook must be a
+    near-tie of the reference (margin < 0.05 between its two nearest codewords); later codebooks quantize a
+    residual that already differs, so they are not compared. The fully-identical-frame fraction is a floor,
+    not the criterion: the encoder's latents differ from fp32 by ~1e-3 relative (f16 activations between the
+    layers), and one near-tie flip changes every later codebook of that frame; the measured fraction is
+    written to gpurun_out/dac_encode_frac.json on the GPU box."""
+    import json
+    import os
     from zonos_vibes_amd.autoencoder import DACAutoencoder
     ae = DACAutoencoder("cuda")
     wav = gold["wav"].cuda()
@@ -96,6 +105,9 @@ def test_hip_encode_matches_reference(gold, weights):
     codes = ae.encode(wav).cpu()
     _, margins = OracleDAC(weights).quantize(gold["latents"])
     frac, bad = near_tie_agreement(codes, gold["codes"], margins, 0.05)
+    if os.path.isdir("gpurun_out"):
+        json.dump(dict(frac_identical_frames=frac, first_diff_not_near_tie=len(bad), latent_max_err=err,
+                       latent_max=ref_lat.abs().max().item()), open("gpurun_out/dac_encode_frac.json", "w"))
     assert not bad, bad[:5]
     assert frac >= 0.5
 

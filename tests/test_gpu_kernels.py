@@ -323,6 +323,29 @@ def test_attention_whole_query_variant_bit_identical_to_chunked(hq, hkv):
                      vc[[0, 6, 10, 14, R - 1]], [positions[i] for i in (0, 6, 10, 14, R - 1)], hq=hq, hkv=hkv)
 
 
+@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("hq,hkv", [(16, 4), (4, 1), (8, 4)])
+def test_attention_split_launch_variants_bit_identical_to_one_launch(hq, hkv, variant):
+    """Variant 2 (scores + maxima launch, then the finish launch, no waiting inside either) and variant 3 (the
+    same, the merge as a third launch) against variant 1 (one launch, maxima exchanged by granules): identical
+    bits at chunk / block edges and at C5 lengths, with a KV-row table, launched twice (the state a launch
+    leaves must not leak into the next)."""
+    hd, smax = 128, 5784
+    positions = [0, 1, 127, 128, 511, 512, 513, 1023, 1279, 1280, 2047, 2049, 3200, 4100, 5775]
+    R = len(positions)
+    kc = rnd(R, hkv, smax, hd, seed=63)
+    vc = rnd(R, hkv, smax, hd, seed=64)
+    q = rnd(R + 2, hq * hd, scale=3.0, seed=65)
+    rows = list(range(R)) + [3, R - 1]
+    pos = positions + [5000, 17]
+    ref = _attention(q, kc, vc, pos, kv_rows=rows, hq=hq, hkv=hkv, variant=1)
+    got = _attention(q, kc, vc, pos, kv_rows=rows, hq=hq, hkv=hkv, variant=variant)
+    assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
+    pick = [0, 6, 12, R - 1, R]
+    _check_attention(got[pick], q[pick], kc, vc, [pos[i] for i in pick], kv_rows=[rows[i] for i in pick], hq=hq,
+                     hkv=hkv)
+
+
 def test_attention_long_context_c5_positions():
     """C5 voice-clone lengths: P = 430 prefix frames + 5168 new ones reach ~5.8k positions, 12
     blocks of 512 keys chained through the cross-block maxima and merged in block order."""

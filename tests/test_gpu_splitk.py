@@ -76,3 +76,33 @@ def test_splitk_fused_layernorm_bit_identical(M, K):
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
     assert torch.equal(got_n, ref_n), (got_n != ref_n).nonzero()[:4].tolist()
+
+
+def test_engine_splitk_and_attention_prefetch_bit_identical():
+    """Engine level: 8 utterances through generate_batch on 8 slots -- the prefill's out_proj / fc2
+    at M = 2 S rows and the 16-row decode steps take the split-K GEMMs (with the fused LayerNorm) and the chunked
+    attention launch with its prefetch role by default -- against the same run with split-K off (the GEMV plan)
+    and with the prefetch role off: identical codes and identical final logits."""
+    from zonos_vibes_amd.config import transformer_config
+    from zonos_vibes_amd.model import Zonos
+    cfg = transformer_config(2048, 3, 16, 4, 8192)
+    lcs = [40, 33, 57, 40, 21, 64, 48, 30]
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_slots=8, max_seqlen=64 + 40 + 16, max_prefill=64 + 8)
+    e = m.engine
+    g = torch.Generator().manual_seed(5)
+    conds = [(torch.randn(2, lc, 2048, generator=g) * 0.5).to(torch.bfloat16).to(DEV) for lc in lcs]
+
+    def run(**opts):
+        for k, v in opts.items():
+            setattr(e, k, v)
+        e._build_plan()
+        out = m.generate_batch(conds, max_new_tokens=40, sampling_params=dict(temperature=0.0), seeds=list(range(8)),
+                               max_slots=8)
+        return [c.cpu() for c in out], e.logits.clone()
+
+    ref_codes, ref_logits = run(attn_prefetch_blocks=256)
+    assert e._use_splitk(*e._gemv(e.w["layers"][0]["fc2"], e.h, 16, 2048, 8192, _lib().EPI_RESIDUAL, e.x, 2048))
+    for opts in (dict(splitk_rows=0, splitk_o_rows=0), dict(splitk_rows=16, splitk_o_rows=16, attn_prefetch_blocks=0)):
+        codes, logits = run(**opts)
+        assert all(torch.equal(a, b) for a, b in zip(codes, ref_codes)), opts
+        assert torch.equal(logits, ref_logits), opts

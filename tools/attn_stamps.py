@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from zonos_vibes_amd import _lib  # noqa: E402
 
 HD, G, HKV, HQ = 128, 4, 4, 16
+VARIANT = int(os.environ.get("ATTN_VARIANT", "1"))  # 2: the scores / finish pair (stamps of the finish launch)
 
 
 def run(pos_list, slots=1, reps=20):
@@ -48,7 +49,7 @@ def run(pos_list, slots=1, reps=20):
                 kc, vt = kcs[(it + k) % nrot], vts[(it + k) % nrot]
                 _lib.check(L.zmi_attention_variant(q.data_ptr(), HQ * HD, kc.data_ptr(), vt.data_ptr(), None,
                                                    rp.data_ptr(), rows, HQ, HKV, HD, smax, smax - 1, out.data_ptr(),
-                                                   HQ * HD, po.data_ptr(), plm.data_ptr(), work.data_ptr(), 1,
+                                                   HQ * HD, po.data_ptr(), plm.data_ptr(), work.data_ptr(), VARIANT,
                                                    torch.cuda.current_stream().cuda_stream))
             torch.cuda.synchronize()
             s = st.cpu()

@@ -59,7 +59,8 @@ def main():
                 if kind == "gemv":
                     e._run_gemv(item)
                 elif kind == "attn":
-                    e._attention(item, e.q, rows, None, e.row_pos, e.smax - 1, e.attn)
+                    i, pf = item if isinstance(item, tuple) else (item, None)
+                    e._attention(i, e.q, rows, None, e.row_pos, e.smax - 1, e.attn, pf)
         e.stream.synchronize()
     st = buf.view(64, 4096, 8).cpu()
     for s, name in enumerate(names):

@@ -5,6 +5,11 @@
 //   0 attn     one 4-wave workgroup per (unit, chunk), the attention kernel's loads (K: 16 keys x 64 B per
 //              instruction, V^T: 16 dim rows x 64 B), all issued at once
 //   1 linear   same workgroups and bytes, 1 KiB-contiguous instructions (K: 4 keys, V^T: 4 dim rows)
+//   3 konly    the attention's K loads only;  4 vonly  its V^T loads only;  5 vlin  V^T only, 1 KiB-contiguous
+//              instructions (4 dim rows x 256 B)
+//   6 vtile    V^T only, stored in 128-position tiles ([unit][tile][128 dims][128 positions]: a chunk's V is one
+//              contiguous 32 KiB), the attention's per-instruction shape (16 dim rows x 64 B)
+//   7 vfinish  mode 4 plus the finish launch's other reads: 2 KiB of scores and the maxima of the chunks before
 //   2 stream   persistent: gridDim workgroups walk the chunks (c = blockIdx, + gridDim), the attention
 //              loads of the next chunk issued before the current one is folded (2 chunks in flight)
 // Occupancy is capped by the dynamic LDS size the driver passes. Built by tools/kv_probe.py.
@@ -51,6 +56,54 @@ __global__ __launch_bounds__(256) void probe_attn(Args a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) x ^= fold(kf[i]) ^ fold(vf[i]);
   if (x == 0x9e3779b9u) pad[threadIdx.x] = 1;  // never (keeps the LDS allocation)
+  a.out[blockIdx.x * 256 + threadIdx.x] = x;
+}
+
+template <int WHICH>  // 3 K only, 4 V^T only, 5 V^T linear, 6 V^T tiled, 7 V^T + finish reads
+__global__ __launch_bounds__(256) void probe_half(Args a) {
+  extern __shared__ char pad[];
+  const int unit = blockIdx.x / a.nch, c = blockIdx.x % a.nch;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c16 = lane & 15, h4 = lane >> 4;
+  const size_t base = (size_t)unit * a.smax * HD;
+  const int key0 = c * CH, last = min(key0 + CH - 1, a.pos);
+  uint4 f[8];
+  if constexpr (WHICH == 3) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int key = min(key0 + wave * 32 + 16 * tt + c16, last);
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+        f[tt * 4 + db] = *reinterpret_cast<const uint4*>(a.k + base + (size_t)key * HD + 8 * h4 + 32 * db);
+    }
+  } else if constexpr (WHICH == 4 || WHICH == 7) {
+    const int p0 = min(key0 + wave * 32 + 8 * h4, last & ~7);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      f[dt] = *reinterpret_cast<const uint4*>(a.v + base + (size_t)(16 * dt + c16) * a.smax + p0);
+  } else if constexpr (WHICH == 6) {
+    const int p0 = min(key0 + wave * 32 + 8 * h4, last & ~7);
+    const size_t tb = base + (size_t)(p0 / 128) * 128 * 128 + (p0 % 128);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) f[dt] = *reinterpret_cast<const uint4*>(a.v + tb + (size_t)(16 * dt + c16) * 128);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wave * 32 + i * 4 + (lane >> 4);
+      f[i] = *reinterpret_cast<const uint4*>(a.v + base + (size_t)row * a.smax + min(key0 + 8 * (lane & 15), a.pos & ~7));
+    }
+  }
+  uint32_t x = 0;
+  if constexpr (WHICH == 7) {  // the scores slot (2 KiB) and the maxima of chunks 0 .. c (4 B each, stride 8 B)
+    const float* sc = reinterpret_cast<const float*>(a.out) + (size_t)(gridDim.x + blockIdx.x) * 512;
+    if (threadIdx.x < 128) x ^= fold(*reinterpret_cast<const uint4*>(sc + threadIdx.x * 4));
+    const int dep = min((c / 4 + 1) * 4, a.nch);
+    const float* lm = reinterpret_cast<const float*>(a.out) + (size_t)3 * gridDim.x * 512 + (size_t)unit * a.nch * 8;
+    if (threadIdx.x < dep * 4) x ^= __float_as_uint(lm[2 * threadIdx.x + 1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x ^= fold(f[i]);
+  if (x == 0x9e3779b9u) pad[threadIdx.x] = 1;
   a.out[blockIdx.x * 256 + threadIdx.x] = x;
 }
 
@@ -109,7 +162,17 @@ extern "C" int kv_probe(int mode, const void* k, const void* v, void* out, int u
     hipLaunchKernelGGL(probe_attn, dim3(blocks), dim3(256), lds_bytes, s, a);
   else if (mode == 1)
     hipLaunchKernelGGL(probe_linear, dim3(blocks), dim3(256), lds_bytes, s, a);
-  else
+  else if (mode == 2)
     hipLaunchKernelGGL(probe_stream, dim3(grid), dim3(256), lds_bytes, s, a);
+  else if (mode == 3)
+    hipLaunchKernelGGL(probe_half<3>, dim3(blocks), dim3(256), lds_bytes, s, a);
+  else if (mode == 4)
+    hipLaunchKernelGGL(probe_half<4>, dim3(blocks), dim3(256), lds_bytes, s, a);
+  else if (mode == 5)
+    hipLaunchKernelGGL(probe_half<5>, dim3(blocks), dim3(256), lds_bytes, s, a);
+  else if (mode == 6)
+    hipLaunchKernelGGL(probe_half<6>, dim3(blocks), dim3(256), lds_bytes, s, a);
+  else
+    hipLaunchKernelGGL(probe_half<7>, dim3(blocks), dim3(256), lds_bytes, s, a);
   return (int)hipGetLastError();
 }

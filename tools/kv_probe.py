@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--layers", type=int, default=26)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--modes", default="0,1,2")
+    ap.add_argument("--occ", default="2,3,4,6,8")
     args = ap.parse_args()
     if args.build_only or not os.path.exists(SO):
         build()
@@ -44,14 +46,15 @@ def main():
     dev = "cuda"
     rows, p = args.rows, args.pos
     smax = p + 72
-    smax += (-smax) % 8
+    smax += (-smax) % 128  # whole 128-position tiles for mode 6
     units = rows * HKV
     kc = [torch.randn(units, smax, HD, device=dev).to(torch.bfloat16) for _ in range(args.layers)]
     vt = [torch.randn(units, HD, smax, device=dev).to(torch.bfloat16) for _ in range(args.layers)]
     nch = p // 128 + 1
-    out = torch.zeros(max(units * nch, 256 * 16) * 256, dtype=torch.int32, device=dev)
+    out = torch.zeros(max(units * nch, 256 * 16) * 256 * 4, dtype=torch.int32, device=dev)  # mode 7 reads beyond
     s = torch.cuda.current_stream().cuda_stream
     nbytes = units * (p + 1) * HD * 2 * 2
+    names = ["attn", "linear", "stream", "konly", "vonly", "vlin", "vtile", "vfinish"]
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run(mode, occ):
@@ -74,11 +77,12 @@ def main():
             en.synchronize()
             ts.append(st.elapsed_time(en) * 1000.0 / args.layers)
         us = min(ts)
-        print(json.dumps(dict(mode=["attn", "linear", "stream"][mode], wg_per_cu=occ, rows=rows, pos=p, us=round(us, 2),
-                              kv_bytes=nbytes, GBps=round(nbytes / us / 1e3, 1))), flush=True)
+        nb = nbytes // 2 if mode >= 3 else nbytes
+        print(json.dumps(dict(mode=names[mode], wg_per_cu=occ, rows=rows, pos=p, us=round(us, 2),
+                              kv_bytes=nb, GBps=round(nb / us / 1e3, 1))), flush=True)
 
-    for mode in (0, 1, 2):
-        for occ in (2, 3, 4, 6, 8):
+    for mode in [int(m) for m in args.modes.split(",")]:
+        for occ in [int(o) for o in args.occ.split(",")]:
             run(mode, occ)
 
 

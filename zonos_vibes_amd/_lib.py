@@ -121,6 +121,9 @@ _SIGS = {
     "zmi_attention_variant": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                       c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                       c_void_p]),
+    "zmi_attention_pf": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                 ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_max_keys_whole": (c_int, []),
     "zmi_attn_block_max_pos": (c_int, [c_int]),
     "zmi_attn_block": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),

@@ -33,6 +33,7 @@
 #include "zmi_attn_merge.h"
 #include "zmi_attn_ds.h"
 #include "zmi_gemv_impl.h"
+#include "zmi_prefetch.h"
 
 namespace {
 
@@ -43,7 +44,13 @@ constexpr unsigned SPIN_LIMIT = 1u << 20;
 
 
 
-template <int G>
+// MODE 0: one launch, the cross-chunk maxima exchanged by granules while the chunks wait. MODE 1 + MODE 2: two
+// launches with no waiting: 1 computes the chunk's scores and maxima and leaves them in its own partial slots
+// (scores in part_o, maxima in part_lm's M word); 2 forms M_j from those maxima, reads its scores back and
+// finishes as MODE 0 does. MODE 3 is MODE 2 without the ticket: it leaves its chunk partial (plain stores) for
+// attn_merge_kernel, a third launch. All give the same bits: max is exact in any order, every other step is shared
+// code (merge2 performs merge4's operations per element).
+template <int G, int MODE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 : 1, 8))) void attn_kernel(const AttnArgs a) {
   __shared__ float sc[G][CH];
   __shared__ __attribute__((aligned(16))) bf16_t pb[G][CH];
@@ -52,6 +59,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   __shared__ float pmax[NT];
   __shared__ unsigned last_flag;
 
+  if constexpr (MODE == 0) {
+    if ((int)blockIdx.x >= a.n_att) {  // prefetch-only workgroup (zmi_attention_pf), dispatched after the chunks
+      prefetch_body<NT>(a.pf, (int)blockIdx.x - a.n_att, a.n_pf);
+      return;
+    }
+  }
   const int unit = blockIdx.x / a.nch, c = blockIdx.x - unit * a.nch;
   const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -73,6 +86,49 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   // under the K / V loads (98 -> 78 VGPRs: 6 workgroups per CU instead of 4) ----
   __shared__ __attribute__((aligned(16))) bf16_t qs[G == 4 ? G * HD : 8];
   uint4 qf[4];
+  uint4 kf[2][4];
+  uint4 vf[8];
+  float* po = a.part_o + ((size_t)unit * a.nch + c) * G * HD;
+  float* plm = a.part_lm + ((size_t)unit * a.nch + c) * G * 2;
+  if constexpr (MODE >= 2) {
+    // launch 1's maxima of chunks 0..dep-1 and this chunk's scores first, then V^T: loads complete in order, so
+    // M_j is formed while V^T is in flight (one memory round trip, not two)
+    const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
+    const int p0 = min(key0 + wave * 32 + 8 * h4, (last_key & ~7));
+#ifdef ZMI_ATTN_LATE
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
+#endif
+    const float mine = t < dep * G ? lu[2 * t + 1] : -INFINITY;  // e = t = chunk * G + head
+    const float4 sv = t * 4 < G * CH ? ld4(po + t * 4) : float4{0.f, 0.f, 0.f, 0.f};
+#ifndef ZMI_ATTN_LATE
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
+#endif
+    float m = mine;
+    for (int e = t + NT; e < dep * G; e += NT) m = fmaxf(m, lu[2 * e + 1]);  // positions >= 64 NT / G only
+    if (t * 4 < G * CH) *reinterpret_cast<float4*>(&sc[(t * 4) / CH][(t * 4) % CH]) = sv;
+    pmax[t] = m;
+    __syncthreads();
+    if (t < G) {  // thread t gathers head t: entries e = t, t + G, ... hold head t (NT % G == 0)
+      float mm = -INFINITY;
+      for (int e = t; e < NT; e += G) mm = fmaxf(mm, pmax[e]);
+      mj[t] = mm;
+    }
+    __syncthreads();
+    ZMI_ASTAMP(1);
+#ifdef ZMI_ATTN_BCUT  // timing-only build: the finish launch stops once M_j and V^T are in (wrong output)
+    {
+      uint32_t x = 0;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) x ^= vf[dt].x ^ vf[dt].w;
+      if (x == 0x9e3779b9u || t == 0) a.out[(size_t)qi * a.ldo + kh * G * HD + (t & 127)] = (bf16_t)(x & 0xffff);
+      return;
+    }
+#endif
+  } else {
   if constexpr (G == 4) {
     if (wave == 0) zmi_gemv::dma_piece(a.q + (size_t)qi * a.ldq + kh * G * HD + lane * 8, qs);
   } else {
@@ -84,7 +140,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
       if (!real) qf[db] = uint4{0u, 0u, 0u, 0u};
     }
   }
-  uint4 kf[2][4];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int key = min(key0 + wave * 32 + 16 * tt + c16, last_key);
@@ -95,16 +150,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   // V^T fragments for P.V, issued with K so both streams share one memory latency (B operand:
   // dim = 16 dt + c16, positions 32 w + 8 h4 .. +7; groups wholly past the position re-read the
   // last valid group, their keys are masked below)
-  uint4 vf[8];
-  {
+  if constexpr (MODE == 0) {
     const int p0 = min(key0 + wave * 32 + 8 * h4, (last_key & ~7));
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
       vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
   }
 
-  if constexpr (G == 4) {  // the q piece (issued before the 16 K / V loads, which complete after it)
-    if (wave == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (G == 4) {  // the q piece (issued before the 16 K / V loads, or the 8 K loads, which complete after it)
+    if constexpr (MODE == 0) {
+      if (wave == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      if (wave == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
     __syncthreads();
   }
   // ---- scores s = fp32(q . k) * scale (dim blocks in order per key tile); keys past the position are -inf ----
@@ -139,14 +197,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   }
   __syncthreads();
   ZMI_ASTAMP(2);
+  if constexpr (MODE == 1) {  // leave the scores and maxima in the chunk's own partial slots for launch 2
+#pragma unroll
+    for (int e = t * 4; e < G * CH; e += NT * 4) *reinterpret_cast<float4*>(po + e) = *reinterpret_cast<const float4*>(&sc[e / CH][e % CH]);
+    if (t < G) plm[2 * t + 1] = mj[t];
+    return;
+  }
+  }  // MODE != 2
 
   // ---- running maximum M_j = max over the chunks of blocks 0..j: {value, tag} granule exchange ----
   uint64_t* gu = a.gran + (size_t)unit * a.nch * G;
-  if (nc > 1 && t < G) st_wt64(gu + c * G + t, pack_f2(mj[t], 1.0f));  // {value, tag 1.0f}: untorn granule
+  if (MODE == 0 && nc > 1 && t < G) st_wt64(gu + c * G + t, pack_f2(mj[t], 1.0f));  // {value, tag 1.0f}: untorn granule
 #ifdef ZMI_ATTN_NOEXCH  // timing experiment only: wrong numerics
   if (false) {
 #else
-  if (dep > 1) {
+  if (MODE == 0 && dep > 1) {
 #endif
     float m = -INFINITY;
     for (int e = t; e < dep * G; e += NT) {  // e = chunk * G + head
@@ -224,9 +289,30 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   __syncthreads();
 
   // ---- chunk partial (waves in order) ----
-  float* po = a.part_o + ((size_t)unit * a.nch + c) * G * HD;
-  float* plm = a.part_lm + ((size_t)unit * a.nch + c) * G * 2;
   bf16_t* dst = a.out + (size_t)qi * a.ldo + kh * G * HD;
+  if constexpr (MODE == 3) {  // plain stores, 4 dims per thread; attn_merge_kernel merges after the launch
+    for (int e = t * 4; e < G * HD; e += NT * 4) {
+      const int g = e / HD, d = e - g * HD;
+      float4 o = *reinterpret_cast<const float4*>(&opart[0][g][d]);
+#pragma unroll
+      for (int w = 1; w < NWC; ++w) {
+        const float4 p = *reinterpret_cast<const float4*>(&opart[w][g][d]);
+        o.x += p.x;
+        o.y += p.y;
+        o.z += p.z;
+        o.w += p.w;
+      }
+      if (nc == 1) {
+        const float r = 1.0f / lj[g];
+        *reinterpret_cast<uint2*>(dst + e) =
+            uint2{f2bf(o.x * r) | (f2bf(o.y * r) << 16), f2bf(o.z * r) | (f2bf(o.w * r) << 16)};
+      } else {
+        *reinterpret_cast<float4*>(po + e) = o;
+      }
+    }
+    if (nc > 1 && t < G) *reinterpret_cast<float2*>(plm + 2 * t) = float2{lj[t], mj[t]};
+    return;
+  }
   for (int e = t; e < G * HD; e += NT) {
     const int g = e / HD, d = e - g * HD;
     float o = opart[0][g][d];
@@ -245,7 +331,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   ZMI_ASTAMP(5);
   if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nc, &last_flag)) return;
   ZMI_ASTAMP(6);
-  for (int e = t; e < nc * G; e += NT) st_wt64(gu + e, 0ull);  // re-arm (every chunk has polled)
+  if constexpr (MODE == 0)
+    for (int e = t; e < nc * G; e += NT) st_wt64(gu + e, 0ull);  // re-arm (every chunk has polled)
 
   // ---- merge (zmi_attn_merge.h), 4 dims per thread. The partials were stored write-through by
   // their chunks; one agent-scope acquire here, then plain loads (MI355X_MICROARCH.md, Valid forms) ----
@@ -256,12 +343,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   __syncthreads();
   const float* ou = a.part_o + (size_t)unit * a.nch * G * HD;
   const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
-  for (int e = t * 4; e < G * HD; e += NT * 4) {
-    const int g = e / HD, d = e - g * HD;
-    const float4 r = merge4(ou, lu, nc, g, d, G);
-    *reinterpret_cast<uint2*>(dst + e) = uint2{f2bf(r.x) | (f2bf(r.y) << 16), f2bf(r.z) | (f2bf(r.w) << 16)};
+#ifdef ZMI_ATTN_M4
+  if constexpr (false) {
+#else
+  if constexpr (MODE == 2) {  // 2 dims per thread, 16 chunks' loads in flight
+#endif
+    for (int e = t * 2; e < G * HD; e += NT * 2) {
+      const int g = e / HD, d = e - g * HD;
+      const float2 r = merge2<16>(ou, lu, nc, g, d, G);
+      *reinterpret_cast<uint32_t*>(dst + e) = f2bf(r.x) | (f2bf(r.y) << 16);
+    }
+  } else {
+    for (int e = t * 4; e < G * HD; e += NT * 4) {
+      const int g = e / HD, d = e - g * HD;
+      const float4 r = merge4(ou, lu, nc, g, d, G);
+      *reinterpret_cast<uint2*>(dst + e) = uint2{f2bf(r.x) | (f2bf(r.y) << 16), f2bf(r.z) | (f2bf(r.w) << 16)};
+    }
   }
   ZMI_ASTAMP(7);
+}
+
+// third launch of variant 3: one 64-thread workgroup per (unit, query head), 2 dims per thread, the unit's chunk
+// partials (left by attn_kernel<G, 3>) merged as the last-arriving chunk merges in MODE 0 / 2
+template <int G>
+__global__ __launch_bounds__(64) void attn_merge_kernel(const AttnArgs a) {
+  const int unit = blockIdx.x / G, g = blockIdx.x - unit * G;
+  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
+  const int nc = chunks_of(a.pos[qi]);
+  if (nc <= 1) return;  // finished by its only chunk
+  const float* ou = a.part_o + (size_t)unit * a.nch * G * HD;
+  const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
+  const int d = threadIdx.x * 2;
+  const float2 r = merge2<16>(ou, lu, nc, g, d, G);
+  *reinterpret_cast<uint32_t*>(a.out + (size_t)qi * a.ldo + (kh * G + g) * HD + d) = f2bf(r.x) | (f2bf(r.y) << 16);
 }
 
 template <int G, int DS>
@@ -315,6 +429,22 @@ hipError_t launch_ds(const AttnArgs& a, int n_units, int ds, hipStream_t s) {
   }
   return hipGetLastError();
 }
+
+// chunked attention: one launch (MODE 0) or the scores / finish pair (MODE 1, 2)
+template <int G>
+hipError_t launch_chunked(const AttnArgs& a, unsigned blocks, int variant, hipStream_t s) {
+  if (variant == 1) {
+    hipLaunchKernelGGL((attn_kernel<G, 0>), dim3(blocks + a.n_pf), dim3(NT), 0, s, a);
+  } else if (variant == 2) {
+    hipLaunchKernelGGL((attn_kernel<G, 1>), dim3(blocks), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<G, 2>), dim3(blocks), dim3(NT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((attn_kernel<G, 1>), dim3(blocks), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((attn_kernel<G, 3>), dim3(blocks), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((attn_merge_kernel<G>), dim3(blocks / a.nch * G), dim3(64), 0, s, a);
+  }
+  return hipGetLastError();
+}
 }  // namespace
 
 extern "C" int zmi_attention_max_keys_whole(void) { return DS_KEYS; }
@@ -330,6 +460,14 @@ extern "C" int zmi_attention_variant(const void* q, int ldq, const void* k_cache
                                      const int* q_kv_row, const int* q_pos, int n_query, int hq, int hkv, int hd,
                                      int smax, int max_pos, void* out, int ldo, float* part_o, float* part_lm,
                                      void* work, int variant, void* stream) {
+  return zmi_attention_pf(q, ldq, k_cache, v_cache, q_kv_row, q_pos, n_query, hq, hkv, hd, smax, max_pos, out, ldo,
+                          part_o, part_lm, work, variant, nullptr, stream);
+}
+
+extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
+                                const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
+                                int ldo, float* part_o, float* part_lm, void* work, int variant,
+                                const ZmiPrefetch* prefetch, void* stream) {
   if (hd != HD) return zmi_fail_msg("attention: head_dim must be 128");
   if (max_pos >= smax) return zmi_fail_msg("attention: max_pos must be < smax");
   if (smax % 8) return zmi_fail_msg("attention: smax must be a multiple of 8");
@@ -359,15 +497,23 @@ extern "C" int zmi_attention_variant(const void* q, int ldq, const void* k_cache
   a.part_o = part_o;
   a.part_lm = part_lm;
   a.stamps = (unsigned long long*)(wb + w.stamps);
+  a.pf = ZmiPrefetch{};
+  a.n_pf = 0;
+  if (prefetch) {
+    if (zmi_prefetch_invalid(*prefetch)) return zmi_fail_msg("attention: bad prefetch ranges");
+    a.pf = *prefetch;
+    a.n_pf = (a.pf.bytes[0] > 0 || a.pf.bytes[1] > 0) ? a.pf.blocks : 0;
+  }
   hipStream_t s = (hipStream_t)stream;
-  // variant: 0 = library choice, 1 = chunked (any length), 4 / 8 = whole-query kernel with that
-  // many dim slices (max_pos < DS_KEYS). Both give identical bits; the choice is speed only. As its
+  // variant: 0 = library choice, 1 = chunked (any length, one launch), 2 = chunked as the scores / finish
+  // launch pair, 3 = scores / partials / merge launches, 4 / 8 = whole-query kernel with that many dim slices (max_pos < DS_KEYS). All give identical
+  // bits; the choice is speed only. As its
   // own launch the whole-query kernel is bound by one CU's ~40 GB/s of K reads (C2 decode: 8.3 /
   // 10.1 / 15.1 us at positions 300 / 591 / 1000 against 10.4 / 10.6 / 10.8 chunked), so the
   // library picks the chunked kernel; the whole-query form pays off where its K/V loads overlap
   // the QKV projection (zmi_attn_block).
   if (variant == 0) variant = 1;
-  if (variant != 1) {
+  if (variant < 1 || variant > 3) {
     a.stamps = nullptr;  // the diagnostic stamp area is laid out for the chunked grid
     if (max_pos >= DS_KEYS) return zmi_fail_msg("attention: the whole-query variant covers positions < 1280");
     if ((int64_t)n_query * hkv * variant > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
@@ -379,18 +525,21 @@ extern "C" int zmi_attention_variant(const void* q, int ldq, const void* k_cache
       case 4: e = launch_ds<4>(a, n_units, variant, s); break;
       default: return zmi_fail_msg("attention: unsupported GQA group (1, 2, 4)");
     }
-    if (e == hipErrorInvalidValue) return zmi_fail_msg("attention: variant must be 0, 1, 4 or 8");
+    if (e == hipErrorInvalidValue) return zmi_fail_msg("attention: variant must be 0, 1, 2, 3, 4 or 8");
     ZMI_CHECK(e);
     return 0;
   }
   const int64_t blocks = (int64_t)n_query * hkv * a.nch;
-  if (blocks > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
+  if (blocks + a.n_pf > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
+  a.n_att = (int)blocks;
+  if (variant != 1) a.n_pf = 0;  // the split-launch forms take no prefetch role
+  hipError_t e;
   switch (g) {
-    case 1: hipLaunchKernelGGL(attn_kernel<1>, dim3((unsigned)blocks), dim3(NT), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(attn_kernel<2>, dim3((unsigned)blocks), dim3(NT), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(attn_kernel<4>, dim3((unsigned)blocks), dim3(NT), 0, s, a); break;
+    case 1: e = launch_chunked<1>(a, (unsigned)blocks, variant, s); break;
+    case 2: e = launch_chunked<2>(a, (unsigned)blocks, variant, s); break;
+    case 4: e = launch_chunked<4>(a, (unsigned)blocks, variant, s); break;
     default: return zmi_fail_msg("attention: unsupported GQA group (1, 2, 4)");
   }
-  ZMI_CHECK(hipGetLastError());
+  ZMI_CHECK(e);
   return 0;
 }

@@ -18,6 +18,7 @@
 
 #pragma once
 #include "zmi_common.h"
+#include "zmi_kernels.h"
 #include "zmi_attn_merge.h"
 
 // Diagnostic build only (-DZMI_ATTN_STAMPS, tools/attn_stamps.py): thread 0 of every workgroup
@@ -52,6 +53,8 @@ struct AttnArgs {
   float* part_o;       // [unit][nch][G][HD]
   float* part_lm;      // [unit][nch][G][2]   l, M_j
   unsigned long long* stamps;  // diagnostic build only
+  ZmiPrefetch pf;      // chunked kernel, one-launch form: prefetch-only workgroups after the n_att chunk ones
+  int n_att, n_pf;
 };
 
 __device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_t c) {

@@ -78,6 +78,52 @@ __device__ __forceinline__ float4 merge4(const float* o, const float* lm, int nc
   return float4{acc.x * r, acc.y * r, acc.z * r, acc.w * r};
 }
 
+// merge4's arithmetic for dims d, d+1 (the same operations per element, so the same bits), MG chunks' loads in
+// flight at a time
+template <int MG>
+__device__ __forceinline__ float2 merge2(const float* o, const float* lm, int nc, int g, int d, int g_heads) {
+  const size_t os = (size_t)g_heads * HD, ls = (size_t)g_heads * 2;
+  float2 acc = {0.f, 0.f}, ob = acc;
+  float l = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
+  for (int c0 = 0; c0 < nc; c0 += MG) {
+    float2 ov[MG], lv[MG];
+#pragma unroll
+    for (int u = 0; u < MG; ++u) {
+      const int cc = min(c0 + u, nc - 1);  // clamped loads past the end are never used
+      ov[u] = ld2(o + cc * os + (size_t)g * HD + d);
+      lv[u] = ld2(lm + cc * ls + (size_t)g * 2);
+    }
+#pragma unroll
+    for (int u = 0; u < MG; ++u) {
+      const int cc = c0 + u;
+      if (cc >= nc) continue;  // (a break here would index ov / lv dynamically: scratch)
+      if (cc % CPB == 0) {
+        ob = ov[u];
+        lb = lv[u].x;
+        mb = lv[u].y;
+      } else {
+        ob.x += ov[u].x;
+        ob.y += ov[u].y;
+        lb += lv[u].x;
+      }
+      if (cc % CPB == CPB - 1 || cc == nc - 1) {
+        if (cc < CPB) {
+          acc = ob;
+          l = lb;
+        } else {
+          const float et = expf(mprev - mb);
+          l = lb + et * l;
+          acc.x = acc.x * et + ob.x;
+          acc.y = acc.y * et + ob.y;
+        }
+        mprev = mb;
+      }
+    }
+  }
+  const float r = 1.0f / l;
+  return float2{acc.x * r, acc.y * r};
+}
+
 // Chunks of the query at position pos (pos < 0: inactive row, 0 chunks).
 __device__ __forceinline__ int chunks_of(int pos) { return pos < 0 ? 0 : pos / CH + 1; }
 

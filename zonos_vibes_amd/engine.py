@@ -123,6 +123,11 @@ class HipEngine:
         # (256, + 4-8 MB), 966 (256, + 16 MB), 974 (512, + 8 MB) (profiles/r03_prefetch_ab.jsonl)
         self.prefetch_blocks = 256
         self.prefetch_fc1_mb = 8
+        # the same prefetch role in the separate chunked attention launch (steps of > 8 rows, positions past the
+        # fused forms' reach): workgroups at the end of its grid read out_proj's weights and the first
+        # `attn_prefetch_fc1_mb` MB of fc1's while the chunks exchange maxima and merge (0 blocks = off)
+        self.attn_prefetch_blocks = 0
+        self.attn_prefetch_fc1_mb = 8
         # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
         # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
         self.prefetch_second = "fc1"
@@ -496,7 +501,14 @@ class HipEngine:
                     plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form))))
                 else:
                     plan.append(("gemv", qkv))
-                    plan.append(("attn", i))
+                    apf = None
+                    if self.attn_prefetch_blocks > 0:
+                        apf = _lib.Prefetch()
+                        apf.ptr[0], apf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
+                        apf.ptr[1] = lw["fc1"].data_ptr()
+                        apf.bytes[1] = min(lw["fc1"].numel() * 2, int(self.attn_prefetch_fc1_mb * 2 ** 20))
+                        apf.sink, apf.blocks = self.blk_err[2:].data_ptr(), self.attn_prefetch_blocks
+                    plan.append(("attn", (i, apf)))
                 if self._use_ffn_engine(rows):
                     plan.append(("ffneng", self._ffn_engine_args(lw, i, rows)))
                     continue
@@ -533,12 +545,12 @@ class HipEngine:
             self._plans[(rows, form)] = plan
         return self._plans[(rows, form)]
 
-    def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out):
-        _lib.check(self.lib.zmi_attention_variant(
+    def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out, pf=None):
+        _lib.check(self.lib.zmi_attention_pf(
             q.data_ptr(), self.H * self.hd, self.kc[i].data_ptr(), self.vc[i].data_ptr(), _lib.ptr(row_kv),
             row_pos.data_ptr(), n_query, self.H, self.Hkv, self.hd, self.smax, max_pos, out.data_ptr(), self.H * self.hd,
-            self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(), self.attn_variant, self.sptr),
-            "attention")
+            self.attn_o.data_ptr(), self.attn_lm.data_ptr(), self.attn_work.data_ptr(), self.attn_variant,
+            None if pf is None else ctypes.byref(pf), self.sptr), "attention")
 
     def _run_attn_block(self, item):
         a, i, pf, slices = item
@@ -648,7 +660,8 @@ class HipEngine:
                                                        self.eps, self.xn.data_ptr(), self.d, self.sptr), "gemv_splitk_ln")
             elif kind == "attn":
                 # decode: query row r caches into KV row r, so no row table (kv_row = NULL)
-                self._attention(item, self.q, rows, None, self.row_pos, self.smax - 1, self.attn)
+                i, pf = item if isinstance(item, tuple) else (item, None)  # (layer, prefetch) or a KV layer index
+                self._attention(i, self.q, rows, None, self.row_pos, self.smax - 1, self.attn, pf)
             else:  # "call": a prepared launch (hybrid kernels)
                 item()
         self._sample(self.logits, noise, 0, 0, rows // 2)

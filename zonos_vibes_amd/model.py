@@ -149,6 +149,7 @@ class Zonos:
                     break
         if bar is not None:
             bar.close()
+        e.check_errors()  # a hand-off that gave up (or a position past a form's reach) must not pass silently
         out = e.read_codes(slot)
         e.release(slot)
         return out
