@@ -125,8 +125,10 @@ class HipEngine:
         self.prefetch_fc1_mb = 8
         # the same prefetch role in the separate chunked attention launch (steps of > 8 rows, positions past the
         # fused forms' reach): workgroups at the end of its grid read out_proj's weights and the first
-        # `attn_prefetch_fc1_mb` MB of fc1's while the chunks exchange maxima and merge (0 blocks = off)
-        self.attn_prefetch_blocks = 0
+        # `attn_prefetch_fc1_mb` MB of fc1's while the chunks exchange maxima and merge (0 blocks = off). C5-shaped
+        # job (8 slots, 2000 new frames): 1.776-1.786 ms per step without, 1.749 with 128 workgroups, 1.760-1.765
+        # with 256 (+ 16 MB of fc1: 1.764); C3 sample unchanged (profiles/r04_attn_prefetch_ab.jsonl)
+        self.attn_prefetch_blocks = 128
         self.attn_prefetch_fc1_mb = 8
         # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
         # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
