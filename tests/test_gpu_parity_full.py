@@ -196,7 +196,8 @@ def test_full_depth_per_layer_error(full):
             elif kind == "gemv":
                 e._run_gemv(item)
             elif kind == "attn":
-                e._attention(item, e.q, 2, None, e.row_pos, e.smax - 1, e.attn)
+                i, pf = item if isinstance(item, tuple) else (item, None)  # (layer, prefetch ranges)
+                e._attention(i, e.q, 2, None, e.row_pos, e.smax - 1, e.attn, pf)
             else:
                 raise AssertionError(kind)
     e.stream.synchronize()
