@@ -457,13 +457,17 @@ def time_default_capacity(dev, n_new: int, ref_codes) -> dict:
     return out
 
 
-def time_long_utterance(dev, n_new: int = 86 * 30) -> dict:
+def time_long_utterance(dev, n_new: int = 86 * 30, engine_opts: dict | None = None) -> dict:
     """One batch-1 utterance at the reference's default generate(max_new_tokens=86 * 30) (model.py:223: 30 s of
     audio, contexts to Lc + 2580 positions): wall-clock RTF of generate() + DAC decode, and the decode step at
     positions across the utterance (HIP events, 64 steps each) with the attention form the plan picks there."""
+    import hashlib
     from zonos_vibes_amd.model import Zonos
     cfg = zonos_v01_transformer()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n_new + 9, max_prefill=LC + 1)
+    for k, v in (engine_opts or {}).items():  # A/B knobs (tools/bench_long.py)
+        setattr(m.engine, k, tuple(v) if isinstance(v, list) else v)
+    m.engine._build_plan()
     cond = cond_tensor(1, cfg.backbone.d_model, dev)
 
     def one():
@@ -485,6 +489,7 @@ def time_long_utterance(dev, n_new: int = 86 * 30) -> dict:
     out = {"config": f"batch 1, Lc {LC}, {n_new} new frames (30 s: the reference default max_new_tokens), greedy, EOS "
                      f"suppressed, + DAC decode", "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3),
            "utterance_ms": round(el * 1e3, 1), "frames": int(codes.shape[-1]),
+           "codes_sha256_16": hashlib.sha256(codes.cpu().numpy().tobytes()).hexdigest()[:16],
            "decode_step_us_by_position": steps}
     del m
     torch.cuda.empty_cache()

@@ -110,7 +110,28 @@ def test_attn_block_bit_identical_to_separate_launches(positions, slices, smax):
                      [positions[i] for i in pick])
 
 
-@pytest.mark.parametrize("slices", [8, 8 | SELF, 8 | SPLIT])
+@pytest.mark.parametrize("positions", [
+    (1024, 1025),                                   # just past the 8-chunk form: one batch-1 step
+    (0, 1, 1535, 1536, 2047, 2048, 2559, 3071),    # block edges of the wide form and its last position
+    (1200, 1201),
+    (3000, 2999),
+])
+@pytest.mark.parametrize("smax", [3072, 3200])
+def test_attn_block_wide_split_bit_identical_to_separate_launches(positions, smax):
+    """The 24-chunk split form (batch-1 decode steps past the 8-chunk reach, up to position 3071): q, the KV
+    cache writes and the attention output bit-identical to the QKV GEMV + chunked attention launches."""
+    slices = 24 | SPLIT
+    assert max(positions) <= _lib().lib().zmi_attn_block_max_pos(slices) == 3071
+    st = _setup(positions, smax, seed=72)
+    ref = _separate(st)
+    got = _fused(st, slices, reps=3)
+    for name, r, g in zip(("q", "k_cache", "v_cache"), ref[:3], got[:3]):
+        assert torch.equal(r, g), name
+    assert torch.equal(ref[3], got[3]), "attention output"
+    _check_attention(got[3][:2], got[0][:2], got[1][:2], got[2][:2].transpose(-1, -2).contiguous(), list(positions[:2]))
+
+
+@pytest.mark.parametrize("slices", [8, 8 | SELF, 8 | SPLIT, 24 | SPLIT])
 def test_attn_block_refuses_positions_past_its_reach(slices):
     """A row past the form's last position sets the error word instead of reading past its K / V reach."""
     L = _lib()

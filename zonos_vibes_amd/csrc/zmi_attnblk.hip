@@ -37,7 +37,10 @@ constexpr int QG = 2, QW = 4, QNL = 8, QRT = 16;  // the projection role's gemv_
 static_assert(QG * QW == DNW, "both roles run the same block size");
 constexpr int XG = 4;                         // query heads per kv head
 constexpr int QKV_GRAN = (XG + 2) * HD / 2;   // q pairs | k pairs | v pairs per (row, kv head)
-constexpr int GRAN_STRIDE = QKV_GRAN + XG * DS_KEYS;  // + the score granules [XG][DS_KEYS]
+constexpr int XC_CH_MAX = 24;                 // widest chunk-split form (chunk workgroups per unit)
+constexpr int XC_WORDS_MAX = 3 * XC_CH_MAX * XG + XC_CH_MAX * XG * HD;  // its granules (layout below)
+// + the score granules [XG][DS_KEYS] of the score-exchange forms, or the chunk-split form's granules
+constexpr int GRAN_STRIDE = QKV_GRAN + (XG * DS_KEYS > XC_WORDS_MAX ? XG * DS_KEYS : XC_WORDS_MAX);
 constexpr int NT = DNW * 64;
 constexpr unsigned XS_SPIN = 1u << 16;
 
@@ -761,13 +764,19 @@ __device__ __forceinline__ void xr_body(const AttnArgs& a, int n_units, int b, c
 // granule hand-offs between the chunks of a query, both small: the chunk maxima (4 per chunk: M_j of
 // the chunk's block), then each chunk's P.V partial, l and M_j, of which workgroup c merges dims
 // 16 c .. 16 c + 15 (zmi_attn_merge.h's recursion). Workgroups of chunks past the position only merge.
-// Positions < XC_KEYS. Granules (after the unit's q / K / V pairs, tag = position + 1): GM [chunk][head]
-// maxima, GL [chunk][head] l, GB [chunk][head] M_j, GO [chunk][head][dim] P.V partials.
-constexpr int XC_CH = 8;                  // chunk workgroups per (query, kv head)
-constexpr int XC_KEYS = XC_CH * CH;       // 1024 keys (positions 0 .. 1023)
-constexpr int XC_GM = 0, XC_GL = XC_GM + XC_CH * XG, XC_GB = XC_GL + XC_CH * XG, XC_GO = XC_GB + XC_CH * XG;
-constexpr int XC_GWORDS = XC_GO + XC_CH * XG * HD;
-static_assert(XC_GWORDS <= XG * DS_KEYS, "the chunk-split granules share the score-granule area");
+// Positions < XCH x 128 for XCH chunk workgroups per (query, kv head): 8 (positions < 1024, the C2 form) or 24
+// (< 3072, batch-1 utterances past the 8-chunk reach). Granules (after the unit's q / K / V pairs, tag =
+// position + 1): GM [chunk][head] maxima, GL [chunk][head] l, GB [chunk][head] M_j, GO [chunk][head][dim] P.V
+// partials. Workgroups 0..7 merge (16 dims each) whatever XCH is.
+template <int XCH>
+struct XcG {
+  static constexpr int KEYS = XCH * CH;
+  static constexpr int GM = 0, GL = GM + XCH * XG, GB = GL + XCH * XG, GO = GB + XCH * XG;
+  static constexpr int WORDS = GO + XCH * XG * HD;
+  static_assert(WORDS <= GRAN_STRIDE - QKV_GRAN, "the chunk-split granules fit the unit's area");
+  static_assert(XCH >= HD / 16 && XCH % CPB == 0 && XCH <= XC_CH_MAX, "8 merging workgroups; whole 512-key blocks");
+};
+constexpr int XC_KEYS = XcG<8>::KEYS;  // the 8-chunk form's reach (1024 keys)
 static_assert(CH == 128 && DNW == 8, "eight waves: one 16-key score tile each over a 128-key chunk");
 
 struct XcImg {
@@ -779,7 +788,10 @@ struct XcImg {
   static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
 };
 
+template <int XCH>
 __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
+  using X = XcG<XCH>;
+  constexpr int XC_CH = XCH, XC_GM = X::GM, XC_GL = X::GL, XC_GB = X::GB, XC_GO = X::GO;
   float(&sc)[XG][CH] = *reinterpret_cast<float(*)[XG][CH]>(smem + XcImg::SC);
   bf16_t(&pb)[XG][CH] = *reinterpret_cast<bf16_t(*)[XG][CH]>(smem + XcImg::PB);
   float(&opart)[CPG][XG][HD] = *reinterpret_cast<float(*)[CPG][XG][HD]>(smem + XcImg::OP);
@@ -792,7 +804,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
   const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
   const int pos = a.pos[qi];
   if (pos < 0) return;
-  if (pos >= XC_KEYS) {  // the engine never launches this form past its capacity; refuse, don't read past it
+  if (pos >= X::KEYS) {  // the engine never launches this form past its capacity; refuse, don't read past it
     if (threadIdx.x == 0) give_up(a);
     return;
   }
@@ -920,28 +932,32 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
         st_wt64(gx + XC_GM + c * XG + lane, (uint64_t)__float_as_uint(mine) | tag64);
       }
       const int j = c / CPB, dep = min((j + 1) * CPB, nc);
-      const int cc = lane / XG, g = lane - cc * XG;
       float v = -INFINITY;
-      if (lane < dep * XG) {
-        if (cc == c) {
-          v = g == 0 ? m[0] : (g == 1 ? m[1] : (g == 2 ? m[2] : m[3]));
-        } else {
-          uint64_t w = ld_wt64(gx + XC_GM + lane);
-          for (unsigned spins = 0; tag_of(w) != tag; ++spins) {
-            if (spins > XS_SPIN) {
-              give_up(a);
-              break;
+#pragma unroll
+      for (int h = 0; h < (XCH * XG + 63) / 64; ++h) {  // entry e = chunk x XG + head; e and e + 64: one head
+        const int e = lane + 64 * h, cc = e / XG, g = e - cc * XG;
+        if (e < dep * XG) {
+          if (cc == c) {
+            v = fmaxf(v, g == 0 ? m[0] : (g == 1 ? m[1] : (g == 2 ? m[2] : m[3])));
+          } else {
+            uint64_t w = ld_wt64(gx + XC_GM + e);
+            for (unsigned spins = 0; tag_of(w) != tag; ++spins) {
+              if (spins > XS_SPIN) {
+                give_up(a);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+              w = ld_wt64(gx + XC_GM + e);
             }
-            __builtin_amdgcn_s_sleep(2);
-            w = ld_wt64(gx + XC_GM + lane);
+            v = fmaxf(v, __uint_as_float((uint32_t)w));
           }
-          v = __uint_as_float((uint32_t)w);
         }
       }
-      // max over the chunks of each head: lanes g, g + 4, ..., g + 28 (dep <= 8 chunks)
+      // max over the chunks of each head: lanes g, g + 4, ..., g + 60 (exact in any order)
       v = fmaxf(v, __shfl_xor(v, 4));
       v = fmaxf(v, __shfl_xor(v, 8));
       v = fmaxf(v, __shfl_xor(v, 16));
+      if constexpr (XCH * XG > 32) v = fmaxf(v, __shfl_xor(v, 32));
       if (lane < XG) mj[lane] = v;
     }
     __syncthreads();
@@ -1004,16 +1020,17 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
   }
   // (8) dims 16 c .. + 15 of the unit's output: every chunk's partial, l and M_j (gathered), the block
   // recursion of zmi_attn_merge.h, one thread per (head, dim)
-  if (t < XG * 16) {
+  if (c < HD / 16 && t < XG * 16) {
     const int g = t >> 4, d = 16 * c + (t & 15);
     uint64_t ov[XC_CH], lv[XC_CH], mv[XC_CH / CPB];
-    unsigned pend = 0;
+    static_assert(2 * XC_CH + XC_CH / CPB <= 64, "one pending bit per granule");
+    uint64_t pend = 0;
 #pragma unroll
     for (int k = 0; k < XC_CH; ++k)
-      if (k < nc) pend |= 3u << (2 * k);
+      if (k < nc) pend |= 3ull << (2 * k);
 #pragma unroll
     for (int j = 0; j < XC_CH / CPB; ++j)
-      if (j * CPB < nc) pend |= 1u << (2 * XC_CH + j);
+      if (j * CPB < nc) pend |= 1ull << (2 * XC_CH + j);
     for (unsigned spins = 0; pend; ++spins) {
 #pragma unroll
       for (int k = 0; k < XC_CH; ++k) {
@@ -1025,12 +1042,12 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
         if ((pend >> (2 * XC_CH + j)) & 1) mv[j] = ld_wt64(gx + XC_GB + j * CPB * XG + g);
 #pragma unroll
       for (int k = 0; k < XC_CH; ++k) {
-        if (((pend >> (2 * k)) & 1) && tag_of(ov[k]) == tag) pend &= ~(1u << (2 * k));
-        if (((pend >> (2 * k + 1)) & 1) && tag_of(lv[k]) == tag) pend &= ~(1u << (2 * k + 1));
+        if (((pend >> (2 * k)) & 1) && tag_of(ov[k]) == tag) pend &= ~(1ull << (2 * k));
+        if (((pend >> (2 * k + 1)) & 1) && tag_of(lv[k]) == tag) pend &= ~(1ull << (2 * k + 1));
       }
 #pragma unroll
       for (int j = 0; j < XC_CH / CPB; ++j)
-        if (((pend >> (2 * XC_CH + j)) & 1) && tag_of(mv[j]) == tag) pend &= ~(1u << (2 * XC_CH + j));
+        if (((pend >> (2 * XC_CH + j)) & 1) && tag_of(mv[j]) == tag) pend &= ~(1ull << (2 * XC_CH + j));
       if (!pend) break;
       if (spins > XS_SPIN) {
         give_up(a);
@@ -1041,7 +1058,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
     float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
 #pragma unroll
     for (int k = 0; k < XC_CH; ++k) {
-      if (k >= nc) break;
+      if (k >= nc) continue;  // (not break: the unrolled arrays stay in registers)
       const float o = __uint_as_float((uint32_t)ov[k]), lk = __uint_as_float((uint32_t)lv[k]);
       if (k % CPB == 0) {
         ob = o;
@@ -1085,7 +1102,7 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
     if constexpr (FORM == FORM_SELF)
       xr_body<S>(at, n_units, b - n_qkv, smem, gran);
     else if constexpr (FORM == FORM_SPLIT)
-      xc_body(at, n_units, b - n_qkv, smem, gran);
+      xc_body<S>(at, n_units, b - n_qkv, smem, gran);
     else
       xs_body<S>(at, n_units, b - n_qkv, smem, gran);
   } else
@@ -1097,9 +1114,11 @@ hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArg
                         const ZmiPrefetch& pf, hipStream_t s) {
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
+  // (the wide chunk-split form with co-resident workgroups instead measured the same: profiles/r04_split24_ab.jsonl)
+  const size_t spread = zmi_gemv::LDS_MAX / 2 + 1024;
   const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, PRO),
                                FORM == FORM_SELF ? XrImg<S>::BYTES : (FORM == FORM_SPLIT ? XcImg::BYTES : XsImg<S>::BYTES),
-                               zmi_gemv::LDS_MAX / 2 + 1024});
+                               spread});
   if (lds > zmi_gemv::LDS_MAX) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S, PRO, FORM>),
@@ -1166,11 +1185,11 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   using zmi_gemv::PRO_LN;
   const int form = (slices & ZMI_ATTNBLK_SPLIT) ? FORM_SPLIT : ((slices & ZMI_ATTNBLK_SELF) ? FORM_SELF : FORM_XS);
   const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
-  if (form == FORM_SPLIT ? sl != 8 : (sl != 4 && sl != 8))
-    return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 | ZMI_ATTNBLK_SPLIT");
+  if (form == FORM_SPLIT ? (sl != 8 && sl != 24) : (sl != 4 && sl != 8))
+    return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 or 24 | ZMI_ATTNBLK_SPLIT");
 #define ZMI_BLK(S_, P_, F_) launch_block<S_, P_, F_>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
 #define ZMI_BLK_P(P_)                                                                                \
-  (form == FORM_SPLIT ? ZMI_BLK(8, P_, FORM_SPLIT)                                                   \
+  (form == FORM_SPLIT ? (sl == 8 ? ZMI_BLK(8, P_, FORM_SPLIT) : ZMI_BLK(24, P_, FORM_SPLIT))           \
                       : form == FORM_SELF ? (sl == 4 ? ZMI_BLK(4, P_, FORM_SELF) : ZMI_BLK(8, P_, FORM_SELF)) \
                                           : (sl == 4 ? ZMI_BLK(4, P_, FORM_XS) : ZMI_BLK(8, P_, FORM_XS)))
   e = addln ? ZMI_BLK_P(PRO_ADDLN) : ZMI_BLK_P(PRO_LN);
@@ -1181,7 +1200,9 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
 }
 
 extern "C" int zmi_attn_block_max_pos(int slices) {
-  return (slices & ZMI_ATTNBLK_SPLIT) ? XC_KEYS - 1 : ((slices & ZMI_ATTNBLK_SELF) ? XR_KEYS - 1 : DS_KEYS - 1);
+  const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
+  return (slices & ZMI_ATTNBLK_SPLIT) ? (sl == 24 ? XcG<24>::KEYS : XC_KEYS) - 1
+                                      : ((slices & ZMI_ATTNBLK_SELF) ? XR_KEYS - 1 : DS_KEYS - 1);
 }
 
 extern "C" int zmi_attn_block(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,

@@ -107,10 +107,13 @@ class HipEngine:
         self.attn_block_slices = 8
         # fused forms tried in order, each where every row's position is below its reach: "split" (one
         # workgroup per 128-key chunk, positions < 1024), "self" (every slice scores all keys, < 1024),
-        # "xs" (slices exchange scores, < 1280); beyond, separate launches. The form is picked per run
-        # of steps from host-side position bounds; all forms give identical bits
-        self.attn_forms = ("split", "xs")
-        # the fused forms for <= `attn_block_rows` rows, "xs" for <= `attn_xs_rows`: C5-shaped steps (1000 frames
+        # "split24" (24 chunk workgroups per (row, kv head), < 3072: batch-1 utterances up to the reference's
+        # default 30 s), "xs" (slices exchange scores, < 1280); beyond, separate launches. The form is picked
+        # per run of steps from host-side position bounds; all forms give identical bits. 30 s batch-1 line:
+        # steps past position 1280 1167-1219 us with separate launches, 1073-1141 with "split24"; at 1161
+        # "split24" 1078.5 against "xs" 1082-1086 (profiles/r04_split24_ab.jsonl)
+        self.attn_forms = ("split", "split24", "xs")
+        # the fused forms for <= `attn_block_rows` rows, "xs" and "split24" for <= `attn_xs_rows`: C5-shaped steps (1000 frames
         # after a 590-position context) at 4 / 8 / 16 rows take 1.232 / 1.516 / 1.902 ms with the fused forms,
         # 1.267 / 1.554 / 1.730 with separate QKV + attention launches, 1.223 / 1.516 / 1.80 without "xs"
         # (profiles/r03_attn_block_rows_ab.jsonl)
@@ -346,6 +349,8 @@ class HipEngine:
         """zmi_attn_block `slices` argument of a fused form."""
         if form == "split":
             return 8 | _lib.ATTNBLK_SPLIT
+        if form == "split24":  # 24 chunk workgroups per (row, kv head): positions < 3072
+            return 24 | _lib.ATTNBLK_SPLIT
         return self.attn_self_slices | _lib.ATTNBLK_SELF if form == "self" else self.attn_block_slices
 
     def _use_ffn_block(self, rows: int) -> bool:
@@ -407,7 +412,7 @@ class HipEngine:
             out.append(("engine", self.dlib.zmi_layer_engine_max_pos()))
         if self.attn_block and rows <= self.attn_block_rows and self.d == 2048 and self.H == 4 * self.Hkv:
             for f in self.attn_forms:
-                if f != "xs" or rows <= self.attn_xs_rows:
+                if f not in ("xs", "split24") or rows <= self.attn_xs_rows:
                     out.append((f, self.lib.zmi_attn_block_max_pos(self._block_slices(f))))
         return out + [("none", 1 << 30)]
 
