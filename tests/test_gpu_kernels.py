@@ -323,13 +323,14 @@ def test_attention_whole_query_variant_bit_identical_to_chunked(hq, hkv):
                      vc[[0, 6, 10, 14, R - 1]], [positions[i] for i in (0, 6, 10, 14, R - 1)], hq=hq, hkv=hkv)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [2, 3, 5])
 @pytest.mark.parametrize("hq,hkv", [(16, 4), (4, 1), (8, 4)])
 def test_attention_split_launch_variants_bit_identical_to_one_launch(hq, hkv, variant):
-    """Variant 2 (scores + maxima launch, then the finish launch, no waiting inside either) and variant 3 (the
-    same, the merge as a third launch) against variant 1 (one launch, maxima exchanged by granules): identical
-    bits at chunk / block edges and at C5 lengths, with a KV-row table, launched twice (the state a launch
-    leaves must not leak into the next)."""
+    """Variant 2 (scores + maxima launch, then the finish launch, no waiting inside either), variant 3 (the
+    same, the merge as a third launch) and variant 5 (one workgroup per 512-key block) against variant 1 (one
+    launch, one workgroup per 128-key chunk, maxima exchanged by granules): identical bits at chunk / block
+    edges and at C5 lengths, with a KV-row table, launched twice (the state a launch leaves must not leak into
+    the next)."""
     hd, smax = 128, 5784
     positions = [0, 1, 127, 128, 511, 512, 513, 1023, 1279, 1280, 2047, 2049, 3200, 4100, 5775]
     R = len(positions)

@@ -68,9 +68,10 @@ def test_generate_batch_full_dims_64_slots_equals_single():
 
 
 def test_attention_form_switch_keeps_codes():
-    """generate() whose positions cross the fused forms' reach (the chunk-split form to position 1023,
-    the score-exchange form to 1279, separate launches beyond): the engine switches graphs at those
-    positions inside one utterance, and the codes equal those of the separate launches throughout."""
+    """generate() whose positions cross the fused forms' reach (the chunk-split form to position 1023, then the
+    24-chunk split form; or, with that form off, the score-exchange form to 1279 and separate launches beyond):
+    the engine switches graphs at those positions inside one utterance, and the codes equal those of the
+    separate launches throughout."""
     from zonos_vibes_amd.model import Zonos
     cfg = transformer_config(2048, 2, 16, 4, 8192)
     lc, n = 1000, 300  # positions 1001 .. 1308
@@ -78,119 +79,15 @@ def test_attention_form_switch_keeps_codes():
     cond = _cond(77, lc, 2048).to(DEV)
     params = dict(temperature=0.0)
     e = m.engine
-    assert [f for f, _ in e._forms(2)][:2] == ["split", "xs"]
-    fused = m.generate(cond, max_new_tokens=n, sampling_params=params, progress_bar=False, chunk=128)
-    e.check_errors()
-    used = sorted({k[1] for k in e._graphs})
-    assert {"split", "xs", "none"} <= set(used), used
+    assert [f for f, _ in e._forms(2)] == ["split", "split24", "xs", "none"]
     e.attn_block = False
     e._build_plan()
     plain = m.generate(cond, max_new_tokens=n, sampling_params=params, progress_bar=False, chunk=128)
-    assert torch.equal(fused, plain)
-
-
-def _ulp(x):
-    return torch.ldexp(torch.ones_like(x), torch.frexp(x.abs().clamp_min(1e-30))[1] - 8)
-
-
-LONG_BOUND_ULPS = 6.0  # allowed |GPU - oracle| score of the oracle's choice, bf16 ulps of its top score
-
-
-def test_long_context_prefix_430_generate_1000_teacher_forced():
-    """Full-width (d 2048, 16 / 4 heads x 128), 2 layers, Lc 32, P = 430 prefix frames, 1,000 new
-    frames, greedy with the repetition penalty, EOS suppressed. Along the oracle's trajectory every
-    decision's GPU score of the oracle's token is within LONG_BOUND_ULPS of the oracle's top score,
-    and the GPU picks the oracle's token wherever the oracle's margin exceeds twice that."""
-    from oracle.zonos_cpu import OracleZonos, apply_delay_pattern, repetition_penalty
-    from tests.helpers import synthetic_weights
-    from zonos_vibes_amd.engine import SamplingParams
-    from zonos_vibes_amd.model import Zonos
-    cfg = transformer_config(2048, 2, 16, 4, 8192)
-    lc, p, n = 32, 430, 1000
-    cond = _cond(7, lc, cfg.backbone.d_model)
-    g = torch.Generator().manual_seed(8)
-    prefix = torch.randint(0, 1024, (1, 9, p), generator=g)
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
-    om = OracleZonos(cfg, synthetic_weights(cfg, zero_eos=True))
-    trace = []
-    om.generate(cond, prefix, max_new_tokens=n, sampling_params=dict(temperature=0.0), trace=trace)
-    dl = om.last_delayed[0].long()
-    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=lc + p + n + 24, max_prefill=lc + p + 8)
-    e = m.engine
-    e.prefill(0, cond.to(DEV), prefix, n, SamplingParams(temperature=0.0))
-    e.stream.synchronize()
-
-    def cfg_logits(rows):
-        c, u = rows[0].float().cpu(), rows[1].float().cpu()
-        lg = u + (c - u) * 2.0
-        lg[..., 1025:] = -torch.inf
-        return lg
-
-    bias = torch.zeros(9, 1026)
-    bias[1:, 1024] = -torch.inf
-    scores = [cfg_logits(e.logits_pre)]
-    dl_dev = dl.to(DEV, torch.int32)
-    for _ in range(len(trace) - 1):
-        with torch.cuda.stream(e.stream):  # the oracle's frames, whatever the GPU sampler chose
-            e.delayed[0, :, : dl.shape[-1]] = dl_dev
-            for k, v in (("active", 1), ("stopping", 0), ("remaining", 2000)):
-                e.st[k][0] = v
-            e.refresh_inputs()
-        o = int(e.st["offset"][0].item())
-        e.step(1, use_graph=False, slots=1)
-        e.stream.synchronize()
-        lg = cfg_logits(e.logits[0:2]) + bias
-        scores.append(repetition_penalty(lg.unsqueeze(0), dl[None, :, : o + 1], 3.0, 2)[0])
-    e.check_errors()
-    init = apply_delay_pattern(torch.cat([prefix, torch.full((1, 9, n), -1)], -1), 1025)[0]
-    rows = []
-    for i in range(min(len(trace), init.shape[1] - p - 1)):
-        f = p + 1 + i  # decision i fills the unknown codebooks of delayed frame f, in order
-        ref = trace[i][0]
-        for mm, k in enumerate((init[:, f] == -1).nonzero().flatten().tolist()):
-            tok = int(dl[k, f])
-            if tok >= 1024:
-                continue
-            t2 = ref[mm].topk(2).values
-            u = float(_ulp(t2[0]))
-            rows.append(dict(err=abs(float(scores[i][mm, tok]) - float(t2[0])) / u,
-                             margin=float(t2[0] - t2[1]) / u, agree=int(scores[i][mm].argmax()) == tok))
-    det = [r for r in rows if r["margin"] > 2 * LONG_BOUND_ULPS]
-    stats = dict(decisions=len(rows), agree=sum(r["agree"] for r in rows), determined=len(det),
-                 determined_agree=sum(r["agree"] for r in det), max_err_ulps=max(r["err"] for r in rows),
-                 mean_err_ulps=sum(r["err"] for r in rows) / len(rows), last_position=lc + p + len(trace))
-    if os.path.isdir("gpurun_out"):
-        json.dump(stats, open("gpurun_out/long_context.json", "w"), indent=1)
-    assert stats["decisions"] > 8000
-    assert stats["determined_agree"] == stats["determined"], stats
-    assert stats["max_err_ulps"] <= LONG_BOUND_ULPS, stats
-
-
-def test_kv_capacity_8_slots_5784_positions():
-    from zonos_vibes_amd.model import Zonos
-    cfg = zonos_v01_transformer()
-    smax_req = 5784
-    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=smax_req, max_prefill=16, max_slots=8)
-    e = m.engine
-    assert e.smax >= smax_req
-    kv_bytes = (e.kc.numel() + e.vc.numel()) * e.kc.element_size()
-    assert kv_bytes == 2 * cfg.backbone.n_layer * 16 * 4 * e.smax * 128 * 2  # 16 rows = 8 CFG slot pairs
-    rows = 16
-    with torch.cuda.stream(e.stream):
-        e.row_pos[:rows] = torch.arange(5760, 5760 + rows, dtype=torch.int32, device=DEV)
-        e.row_kv[:rows] = torch.arange(rows, dtype=torch.int32, device=DEV)
-        e.x[:rows].normal_()
-        e.kc.normal_()
-        e.vc.normal_()
-    e.stream.synchronize()
-    e.pos_hi[:8] = [5760 + rows - 1] * 8  # host position bound (set by a prefill in generate())
-    e.step(1, use_graph=True, slots=8)
-    e.stream.synchronize()
-    e.check_errors()
-    assert torch.isfinite(e.logits[:rows]).all()
-    # the last layer's attention of three rows at ~5.77k keys against the blocking oracle and fp32 SDPA
-    from tests.test_gpu_kernels import _check_attention
-    last = cfg.backbone.n_layer - 1
-    pick = [0, 7, 15]
-    _check_attention(e.attn[pick], e.q[pick], e.kc[last][pick], e.vc[last][pick].transpose(-1, -2).contiguous(),
-                     [5760 + r for r in pick])
+    for forms, want in ((("split", "xs"), {"split", "xs", "none"}), (("split", "split24", "xs"), {"split", "split24"})):
+        e.attn_block, e.attn_forms = True, forms
+        e._build_plan()
+        fused = m.generate(cond, max_new_tokens=n, sampling_params=params, progress_bar=False, chunk=128)
+        e.check_errors()
+        used = {k[1] for k in e._graphs}
+        assert want <= used, (forms, sorted(used))
+        assert torch.equal(fused, plain), forms

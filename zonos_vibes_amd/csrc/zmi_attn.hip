@@ -363,6 +363,215 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   ZMI_ASTAMP(7);
 }
 
+// ---- block form (variant 5): one 8-wave workgroup per (query, kv head, 512-key softmax block) ----
+// Wave w owns keys 64 w .. 64 w + 63 of the block as two 32-key tiles (the chunked kernel's wave unit), so a
+// 128-key chunk is tiles 4 cc .. 4 cc + 3. Every per-chunk operation is the chunked kernel's: the same score
+// MFMA chain, l of chunk cc and head g summed by one wave over lanes L and L + 64, P = bf16(e), P.V per tile
+// from zero, the chunk's tiles summed in tile order, then (zmi_attn_merge.h) the block's chunks in chunk order
+// and the blocks folded by the reference recursion. What changes is who waits: the chunks of a block need no
+// exchange (the block maximum is local), and block j only needs the maxima of blocks 0 .. j - 1, whose
+// workgroups come earlier in the grid; one partial and one ticket per block instead of per chunk. The V^T
+// loads are issued after the scores (the K registers are dead by then), so they run during that wait.
+constexpr int BNW = 8, BNT = BNW * 64;
+constexpr int BTL = BLK / 32;  // 32-key tiles per block
+
+template <int G>
+__global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) void attn_blk_kernel(const AttnArgs a) {
+  __shared__ float sc[G][BLK];
+  __shared__ __attribute__((aligned(16))) bf16_t pb[G][BLK];
+  __shared__ float opart[BTL][G][HD];
+  __shared__ __attribute__((aligned(16))) bf16_t qs[G * HD];
+  __shared__ float mj[G], bmx[G], lch[CPB][G];
+  __shared__ unsigned last_flag;
+
+  if ((int)blockIdx.x >= a.n_att) {  // prefetch-only workgroup (zmi_attention_pf)
+    prefetch_body<BNT>(a.pf, (int)blockIdx.x - a.n_att, a.n_pf);
+    return;
+  }
+  const int nblk = (a.nch + CPB - 1) / CPB;
+  const int unit = blockIdx.x / nblk, j = blockIdx.x - unit * nblk;
+  const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
+  const int pos = a.pos[qi];
+  const int nc = chunks_of(pos), nb = (nc + CPB - 1) / CPB;
+  if (j >= nb) return;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c16 = lane & 15, h4 = lane >> 4;
+  const int key0 = j * BLK;
+  const int nkeys = min(BLK, pos + 1 - key0), last_key = key0 + nkeys - 1;
+  const int ncb = (nkeys + CH - 1) / CH;  // chunks of this block
+  const int kvr = a.kv_row ? a.kv_row[qi] : qi;
+  const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
+
+  if (t < G * HD / 8)
+    *reinterpret_cast<uint4*>(&qs[t * 8]) = *reinterpret_cast<const uint4*>(a.q + (size_t)qi * a.ldq + kh * G * HD + t * 8);
+  uint4 kf[2][2][4];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int key = min(key0 + 32 * (2 * wave + k) + 16 * tt + c16, last_key);
+      const bf16_t* kr = a.k + kvbase + (size_t)key * HD + 8 * h4;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) kf[k][tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
+    }
+  __syncthreads();  // q in LDS
+  // ---- scores (the chunked kernel's chain per 16-key sub-tile); keys past the position are -inf ----
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    f32x4_t st[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const uint4 qv = c16 < G ? *reinterpret_cast<const uint4*>(&qs[c16 * HD + 8 * h4 + 32 * db]) : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) st[tt] = mfma16(qv, kf[k][tt][db], st[tt]);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int key = 32 * (2 * wave + k) + 16 * tt + c16;  // block-local
+      if (h4 == 0) {
+#pragma unroll
+        for (int i = 0; i < G; ++i) sc[i][key] = key < nkeys ? st[tt][i] * a.scale : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- V^T fragments of the wave's two tiles (issued now, landing while the block maxima are exchanged) ----
+  uint4 vf[2][8];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p0 = min(key0 + 32 * (2 * wave + k) + 8 * h4, last_key & ~7);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vf[k][dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
+  }
+  // ---- block maxima (exact in any order), out as {value, tag} granules; M_j = max over blocks 0..j ----
+  if (wave < G) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < BLK / 64; ++i) m = fmaxf(m, sc[wave][lane + 64 * i]);
+    m = wave_max(m);
+    if (lane == 0) bmx[wave] = m;
+  }
+  __syncthreads();
+  uint64_t* gu = a.gran + (size_t)unit * a.nch * G;  // [block][head] in the unit's granule area
+  if (wave == 0) {
+    if (nb > 1 && lane < G) st_wt64(gu + j * G + lane, pack_f2(bmx[lane], 1.0f));
+    float m = lane < G ? bmx[lane] : -INFINITY;
+    for (int e = lane; e < j * G; e += 64) {  // e = block x G + head (64 % G == 0: lane's head is lane % G)
+      uint64_t v = ld_wt64(gu + e);
+      for (unsigned spins = 0; hi_f(v) != 1.0f; ++spins) {
+        if (spins > SPIN_LIMIT) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = ld_wt64(gu + e);
+      }
+      m = fmaxf(m, lo_f(v));
+    }
+#pragma unroll
+    for (int off = G; off < 64; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if (lane < G) mj[lane] = m;
+  }
+  __syncthreads();
+  // ---- e = exp(s - M_j), l per (chunk, head) as the chunked kernel's wave does it, P = bf16(e) ----
+  for (int task = wave; task < CPB * G; task += BNW) {
+    const int cc = task / G, g = task - cc * G;
+    const float M = mj[g];
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < CH / 64; ++i) {
+      const int kk = cc * CH + lane + 64 * i;
+      const float e = kk < nkeys ? expf(sc[g][kk] - M) : 0.f;
+      l += e;
+      pb[g][kk] = (bf16_t)f2bf(e);
+    }
+    l = wave_sum(l);
+    if (lane == 0) lch[cc][g] = l;
+  }
+  __syncthreads();
+  // ---- P.V per 32-key tile (V of keys past the position zeroed) ----
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int tl = 2 * wave + k;
+    uint4 pf = uint4{0u, 0u, 0u, 0u};
+    if (c16 < G) pf = *reinterpret_cast<const uint4*>(&pb[c16][32 * tl + 8 * h4]);
+    const int kbase = 32 * tl + 8 * h4;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint4 v = vf[k][dt];
+      if (kbase + 8 > nkeys) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = kbase + 2 * e < nkeys ? 0x0000ffffu : 0u;
+          const uint32_t hi = kbase + 2 * e + 1 < nkeys ? 0xffff0000u : 0u;
+          w[e] &= lo | hi;
+        }
+        v = uint4{w[0], w[1], w[2], w[3]};
+      }
+      const f32x4_t o = mfma16(pf, v, f32x4_t{0.f, 0.f, 0.f, 0.f});
+      if (h4 == 0) {
+#pragma unroll
+        for (int i = 0; i < G; ++i) opart[tl][i][16 * dt + c16] = o[i];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- the block's partial: chunks' tiles in tile order, then the chunks in chunk order ----
+  float* po = a.part_o + ((size_t)unit * a.nch + j) * G * HD;
+  float* plm = a.part_lm + ((size_t)unit * a.nch + j) * G * 2;
+  bf16_t* dst = a.out + (size_t)qi * a.ldo + kh * G * HD;
+  for (int e = t; e < G * HD; e += BNT) {
+    const int g = e / HD, d = e - g * HD;
+    float ob = 0.f, lb = 0.f;
+    for (int cc = 0; cc < ncb; ++cc) {
+      float o = opart[4 * cc][g][d];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) o += opart[4 * cc + w][g][d];
+      ob = cc == 0 ? o : ob + o;
+      lb = cc == 0 ? lch[0][g] : lb + lch[cc][g];
+    }
+    if (nb == 1)  // one block: finished here (acc = ob, l = lb, as merge4 leaves them)
+      dst[e] = (bf16_t)f2bf(ob * (1.0f / lb));
+    else
+      st_wt(po + e, ob);
+    if (nb > 1 && d == 0) {
+      st_wt(plm + 2 * g, lb);
+      st_wt(plm + 2 * g + 1, mj[g]);
+    }
+  }
+  if (nb == 1) return;
+  if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nb, &last_flag)) return;
+  for (int e = t; e < nb * G; e += BNT) st_wt64(gu + e, 0ull);  // re-arm (every block has read its maxima)
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // ---- fold the blocks (the reference recursion, as merge4 does after its per-block sums) ----
+  const float* ou = a.part_o + (size_t)unit * a.nch * G * HD;
+  const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
+  for (int e = t; e < G * HD; e += BNT) {
+    const int g = e / HD, d = e - g * HD;
+    float acc = 0.f, l = 0.f, mprev = 0.f;
+    for (int b = 0; b < nb; ++b) {
+      const float ob = ou[(size_t)b * G * HD + e];
+      const float2 lm = ld2(lu + (size_t)b * G * 2 + 2 * g);
+      if (b == 0) {
+        acc = ob;
+        l = lm.x;
+      } else {
+        const float et = expf(mprev - lm.y);
+        l = lm.x + et * l;
+        acc = acc * et + ob;
+      }
+      mprev = lm.y;
+    }
+    dst[e] = (bf16_t)f2bf(acc * (1.0f / l));
+  }
+}
+
 // third launch of variant 3: one 64-thread workgroup per (unit, query head), 2 dims per thread, the unit's chunk
 // partials (left by attn_kernel<G, 3>) merged as the last-arriving chunk merges in MODE 0 / 2
 template <int G>
@@ -438,10 +647,12 @@ hipError_t launch_chunked(const AttnArgs& a, unsigned blocks, int variant, hipSt
   } else if (variant == 2) {
     hipLaunchKernelGGL((attn_kernel<G, 1>), dim3(blocks), dim3(NT), 0, s, a);
     hipLaunchKernelGGL((attn_kernel<G, 2>), dim3(blocks), dim3(NT), 0, s, a);
-  } else {
+  } else if (variant == 3) {
     hipLaunchKernelGGL((attn_kernel<G, 1>), dim3(blocks), dim3(NT), 0, s, a);
     hipLaunchKernelGGL((attn_kernel<G, 3>), dim3(blocks), dim3(NT), 0, s, a);
     hipLaunchKernelGGL((attn_merge_kernel<G>), dim3(blocks / a.nch * G), dim3(64), 0, s, a);
+  } else {  // 5: block form, one workgroup per (query, kv head, 512-key block) + the prefetch workgroups
+    hipLaunchKernelGGL((attn_blk_kernel<G>), dim3((unsigned)a.n_att + a.n_pf), dim3(BNT), 0, s, a);
   }
   return hipGetLastError();
 }
@@ -506,14 +717,18 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
   }
   hipStream_t s = (hipStream_t)stream;
   // variant: 0 = library choice, 1 = chunked (any length, one launch), 2 = chunked as the scores / finish
-  // launch pair, 3 = scores / partials / merge launches, 4 / 8 = whole-query kernel with that many dim slices (max_pos < DS_KEYS). All give identical
+  // launch pair, 3 = scores / partials / merge launches, 5 = one workgroup per 512-key block, 4 / 8 = whole-query kernel with that many dim slices (max_pos < DS_KEYS). All give identical
   // bits; the choice is speed only. As its
   // own launch the whole-query kernel is bound by one CU's ~40 GB/s of K reads (C2 decode: 8.3 /
   // 10.1 / 15.1 us at positions 300 / 591 / 1000 against 10.4 / 10.6 / 10.8 chunked), so the
   // library picks the chunked kernel; the whole-query form pays off where its K/V loads overlap
   // the QKV projection (zmi_attn_block).
-  if (variant == 0) variant = 1;
-  if (variant < 1 || variant > 3) {
+  // The block form (5) needs enough (query, kv head) units to fill the chip with one workgroup per 512 keys:
+  // 16 rows x 1500 / 3200 / 5700 keys 19.9 / 31.5 / 56.2 us against 22.2 / 36.9 / 58.4 chunked, 8 rows x 3200
+  // 20.4 against 25.3, 128 rows x 1000 equal, 2 rows x 3200 18.1 against 15.6
+  // (profiles/r04_attn_block_form.jsonl).
+  if (variant == 0) variant = (int64_t)n_query * hkv >= 32 ? 5 : 1;
+  if (variant < 1 || (variant > 3 && variant != 5)) {
     a.stamps = nullptr;  // the diagnostic stamp area is laid out for the chunked grid
     if (max_pos >= DS_KEYS) return zmi_fail_msg("attention: the whole-query variant covers positions < 1280");
     if ((int64_t)n_query * hkv * variant > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
@@ -525,14 +740,14 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
       case 4: e = launch_ds<4>(a, n_units, variant, s); break;
       default: return zmi_fail_msg("attention: unsupported GQA group (1, 2, 4)");
     }
-    if (e == hipErrorInvalidValue) return zmi_fail_msg("attention: variant must be 0, 1, 2, 3, 4 or 8");
+    if (e == hipErrorInvalidValue) return zmi_fail_msg("attention: variant must be 0, 1, 2, 3, 4, 5 or 8");
     ZMI_CHECK(e);
     return 0;
   }
   const int64_t blocks = (int64_t)n_query * hkv * a.nch;
   if (blocks + a.n_pf > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
-  a.n_att = (int)blocks;
-  if (variant != 1) a.n_pf = 0;  // the split-launch forms take no prefetch role
+  a.n_att = variant == 5 ? (int)((int64_t)n_query * hkv * ((a.nch + CPB - 1) / CPB)) : (int)blocks;
+  if (variant != 1 && variant != 5) a.n_pf = 0;  // the split-launch forms take no prefetch role
   hipError_t e;
   switch (g) {
     case 1: e = launch_chunked<1>(a, (unsigned)blocks, variant, s); break;
