@@ -86,9 +86,10 @@ def test_hip_encode_matches_reference(gold, weights):
     The parity criterion is `bad`: in every frame whose codes differ, the FIRST differing codebook must be a
     near-tie of the reference (margin < 0.05 between its two nearest codewords); later codebooks quantize a
     residual that already differs, so they are not compared. The fully-identical-frame fraction is a floor,
-    not the criterion: the encoder's latents differ from fp32 by ~1e-3 relative (f16 activations between the
-    layers), and one near-tie flip changes every later codebook of that frame; the measured fraction is
-    written to gpurun_out/dac_encode_frac.json on the GPU box."""
+    the second criterion: the encoder's latents differ from fp32 by ~1e-3 relative (f16 activations between
+    the layers; measured max 3.2e-4 against a latent range of 0.28), and one near-tie flip would change every
+    later codebook of that frame. Measured on the fixture: every frame identical (gpurun_out/
+    dac_encode_frac.json on the GPU box); required: at least 90 %."""
     import json
     import os
     from zonos_vibes_amd.autoencoder import DACAutoencoder
@@ -109,7 +110,7 @@ def test_hip_encode_matches_reference(gold, weights):
         json.dump(dict(frac_identical_frames=frac, first_diff_not_near_tie=len(bad), latent_max_err=err,
                        latent_max=ref_lat.abs().max().item()), open("gpurun_out/dac_encode_frac.json", "w"))
     assert not bad, bad[:5]
-    assert frac >= 0.5
+    assert frac >= 0.9, frac
 
 
 @pytest.mark.gpu

@@ -388,8 +388,12 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     prefetch_body<BNT>(a.pf, (int)blockIdx.x - a.n_att, a.n_pf);
     return;
   }
-  const int nblk = (a.nch + CPB - 1) / CPB;
-  const int unit = blockIdx.x / nblk, j = blockIdx.x - unit * nblk;
+  // block-major order: the live blocks (j < the row's block count) come first and every unit's blocks spread
+  // over the XCDs (workgroups are dealt round-robin; unit-major order with the KV capacity's 12 blocks put all
+  // live blocks of a C5 step on 4 of the 8 XCDs: 26.8 against 17.1 us at 16 rows x 1000 keys); block j waits
+  // only for blocks 0 .. j - 1 of its unit, which this order dispatches earlier
+  const int n_units = a.n_att / ((a.nch + CPB - 1) / CPB);
+  const int j = blockIdx.x / n_units, unit = blockIdx.x - j * n_units;
   const int qi = unit / a.hkv, kh = unit - qi * a.hkv;
   const int pos = a.pos[qi];
   const int nc = chunks_of(pos), nb = (nc + CPB - 1) / CPB;
@@ -723,10 +727,10 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
   // 10.1 / 15.1 us at positions 300 / 591 / 1000 against 10.4 / 10.6 / 10.8 chunked), so the
   // library picks the chunked kernel; the whole-query form pays off where its K/V loads overlap
   // the QKV projection (zmi_attn_block).
-  // The block form (5) needs enough (query, kv head) units to fill the chip with one workgroup per 512 keys:
-  // 16 rows x 1500 / 3200 / 5700 keys 19.9 / 31.5 / 56.2 us against 22.2 / 36.9 / 58.4 chunked, 8 rows x 3200
-  // 20.4 against 25.3, 128 rows x 1000 equal, 2 rows x 3200 18.1 against 15.6
-  // (profiles/r04_attn_block_form.jsonl).
+  // The block form (5) needs enough (query, kv head) units to fill the chip with one workgroup per 512 keys.
+  // 16 rows at the engine's launch shape (max_pos = the C5 KV capacity 5783) x 1000 / 1600 / 2600 / 5000 keys:
+  // 17.5 / 19.9 / 30.3 / 44.8 us against 21.4 / 26.6 / 32.8 / 52.6 chunked; 8 rows x 3200 20.4 against 25.3;
+  // 128 rows x 1000 equal; 2 rows x 3200 18.1 against 15.6 (profiles/r04_attn_block_form.jsonl).
   if (variant == 0) variant = (int64_t)n_query * hkv >= 32 ? 5 : 1;
   if (variant < 1 || (variant > 3 && variant != 5)) {
     a.stamps = nullptr;  // the diagnostic stamp area is laid out for the chunked grid
