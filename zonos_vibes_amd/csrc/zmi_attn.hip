@@ -406,8 +406,14 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const int kvr = a.kv_row ? a.kv_row[qi] : qi;
   const size_t kvbase = ((size_t)kvr * a.hkv + kh) * a.smax * HD;
 
-  if (t < G * HD / 8)
-    *reinterpret_cast<uint4*>(&qs[t * 8]) = *reinterpret_cast<const uint4*>(a.q + (size_t)qi * a.ldq + kh * G * HD + t * 8);
+  // q: with G = 4 one 1 KiB LDS-DMA piece that lands under the K loads (a load + LDS store would make the wave
+  // wait for q before issuing any K load); smaller groups by plain loads
+  if constexpr (G == 4) {
+    if (wave == 0) zmi_gemv::dma_piece(a.q + (size_t)qi * a.ldq + kh * G * HD + lane * 8, qs);
+  } else {
+    if (t < G * HD / 8)
+      *reinterpret_cast<uint4*>(&qs[t * 8]) = *reinterpret_cast<const uint4*>(a.q + (size_t)qi * a.ldq + kh * G * HD + t * 8);
+  }
   uint4 kf[2][2][4];
 #pragma unroll
   for (int k = 0; k < 2; ++k)
@@ -418,6 +424,9 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 #pragma unroll
       for (int db = 0; db < 4; ++db) kf[k][tt][db] = *reinterpret_cast<const uint4*>(kr + 32 * db);
     }
+  if constexpr (G == 4) {  // the q piece was issued before the 16 K loads, which complete after it
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
   __syncthreads();  // q in LDS
   // ---- scores (the chunked kernel's chain per 16-key sub-tile); keys past the position are -inf ----
 #pragma unroll
