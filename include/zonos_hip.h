@@ -65,11 +65,6 @@ typedef struct ZmiGemvArgs {
   int ld_aux;           /* row stride of aux and res_out (elements)                             */
   const void* aux;      /* ADDLN: bf16 residual rows; GRMS: f32 gate rows z * sigmoid(z)          */
   void* res_out;        /* ADDLN: bf16 [M][ld_aux] new residual, or NULL                         */
-  /* zmi_gemv_launch only (0 = none): pf_blocks prefetch-only workgroups after the GEMV's grid read
-   * pf_ptr[0 .. pf_bytes) once, so the next launch finds those bytes in the Infinity Cache (speed only) */
-  const void* pf_ptr;
-  int64_t pf_bytes;
-  int pf_blocks, pf_reserved;
 } ZmiGemvArgs;
 
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);

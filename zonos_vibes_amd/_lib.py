@@ -44,7 +44,6 @@ class GemvArgs(ctypes.Structure):
         ("smax", c_int), ("hq", c_int), ("hkv", c_int), ("hd", c_int),
         ("rope", c_void_p), ("diag", c_void_p),
         ("pro", c_int), ("ld_aux", c_int), ("aux", c_void_p), ("res_out", c_void_p),
-        ("pf_ptr", c_void_p), ("pf_bytes", ctypes.c_int64), ("pf_blocks", c_int), ("pf_reserved", c_int),
     ]
 
 

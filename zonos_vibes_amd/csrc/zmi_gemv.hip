@@ -60,8 +60,6 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
     return zmi_fail_msg("gemv: GRMS needs ln_w (the norm weight), aux = the f32 gate (ld_aux % 8 == 0), M <= 4");
   if (epi == ZMI_EPI_QKV && (a.hd % 8 || a.smax <= 0 || !a.row_pos || !a.row_kv || !a.rope))
     return zmi_fail_msg("gemv: the QKV epilogue needs row_pos, row_kv, rope, smax and hd % 8 == 0");
-  if (a.pf_bytes < 0 || a.pf_blocks < 0 || a.pf_blocks > 4096 || (a.pf_bytes > 0 && (!a.pf_ptr || a.pf_blocks == 0)))
-    return zmi_fail_msg("gemv: prefetch needs pf_ptr, pf_bytes >= 0 and 1 <= pf_blocks <= 4096");
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   switch (epi) {

@@ -28,7 +28,6 @@
 #include <algorithm>
 #include "zmi_common.h"
 #include "zmi_kernels.h"
-#include "zmi_prefetch.h"
 
 namespace zmi_gemv {
 
@@ -594,13 +593,6 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
 template <int G, int W, int NL, int RT, int PRO, int EPI, int NTW>
 __global__ __launch_bounds__(G * W * 64) void gemv_kernel(const ZmiGemvArgs a, int n_cb, int n_rt, int rpw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.pf_blocks > 0 && (int)blockIdx.x >= (int)gridDim.x - a.pf_blocks) {  // prefetch-only workgroup
-    ZmiPrefetch pf{};
-    pf.ptr[0] = a.pf_ptr;
-    pf.bytes[0] = a.pf_bytes;
-    prefetch_body<G * W * 64>(pf, (int)blockIdx.x - ((int)gridDim.x - a.pf_blocks), a.pf_blocks);
-    return;
-  }
   gemv_body<G, W, NL, RT, PRO, EPI, NTW>(a, n_cb, n_rt, blockIdx.x, smem, QkvFuse{nullptr, 0}, rpw);
 }
 
@@ -882,11 +874,8 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
                             (int)LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
-  const int n_pf = a.pf_bytes > 0 ? a.pf_blocks : 0;
-  if (blocks + n_pf > 0x7fffffff) return hipErrorInvalidValue;
-  ZmiGemvArgs ak = a;
-  ak.pf_blocks = n_pf;
-  hipLaunchKernelGGL(fn, dim3((unsigned)(blocks + n_pf)), dim3(G * W * 64), lds, s, ak, n_cb, n_rt, rpw);
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(G * W * 64), lds, s, a, n_cb, n_rt, rpw);
   return hipGetLastError();
 }
 

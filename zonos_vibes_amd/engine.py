@@ -133,14 +133,6 @@ class HipEngine:
         # with 256 (+ 16 MB of fc1: 1.764); C3 sample unchanged (profiles/r04_attn_prefetch_ab.jsonl)
         self.attn_prefetch_blocks = 128
         self.attn_prefetch_fc1_mb = 8
-        # prefetch roles of the decode GEMVs (zmi_gemv_launch pf_*: `gemv_prefetch_blocks` workgroups after the
-        # GEMV's grid, dispatched as its workgroups retire): fc1 reads the first `fc1_prefetch_mb` MB of fc2's
-        # weights, fc2 the first `fc2_prefetch_mb` MB of the next layer's QKV weights (the heads' after the last
-        # layer); 0 = off. Speed only. Measured neutral on the C2 step (978-979 us with any of fc1 -> 8 / 16 MB of
-        # fc2, fc2 -> 12 MB of the next QKV, both, 256 workgroups; profiles/r04_gemv_prefetch_ab.jsonl): off
-        self.gemv_prefetch_blocks = 128
-        self.fc1_prefetch_mb = 0
-        self.fc2_prefetch_mb = 0
         # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
         # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
         self.prefetch_second = "fc1"
@@ -179,6 +171,8 @@ class HipEngine:
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
+        # generate_batch steps only slots 0 .. the highest busy one (bucketed), not every slot
+        self.batch_shrink = True
         self.slot_greedy = [False] * self.S
         self._plans: dict[tuple, list] = {}
         self._graphs: dict[tuple, int] = {}
@@ -541,12 +535,10 @@ class HipEngine:
                     else:
                         plan.append(("gemv", o_item))
                     xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
-                    f1 = self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F, ln=ln)
-                    self._set_prefetch(f1[0], lw["fc2"], self.fc1_prefetch_mb)
-                    plan.append(("gemv", f1))
+                    plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
+                                                    self.F, ln=ln)))
                 fc2 = self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)
                 last = i + 1 == len(w["layers"])
-                self._set_prefetch(fc2[0], w["heads"] if last else w["layers"][i + 1]["qkv"], self.fc2_prefetch_mb)
                 nxt = (w["nf_w"], w["nf_b"]) if last else (w["layers"][i + 1]["ln1_w"], w["layers"][i + 1]["ln1_b"])
                 if pre and (last or not fused) and self._use_splitk(*fc2) and d == 2048:
                     # the split-K reduce also writes LayerNorm(new x) for the next op (no pre-pass launch)
@@ -561,12 +553,6 @@ class HipEngine:
             plan.append(("gemv", heads))
             self._plans[(rows, form)] = plan
         return self._plans[(rows, form)]
-
-    def _set_prefetch(self, a, weight, mb: float):
-        """A decode GEMV's prefetch role: read the first `mb` MB of `weight` into the Infinity Cache (speed only)."""
-        if mb > 0 and self.gemv_prefetch_blocks > 0:
-            a.pf_ptr, a.pf_bytes = weight.data_ptr(), min(weight.numel() * 2, int(mb * 2 ** 20))
-            a.pf_blocks = self.gemv_prefetch_blocks
 
     def _attention(self, i, q, n_query, row_kv, row_pos, max_pos, out, pf=None):
         _lib.check(self.lib.zmi_attention_pf(

@@ -187,10 +187,16 @@ class Zonos:
                     remaining[s] = mnt[i] + 8
             e.prefill_many(items)  # the free slots' prefills in as few passes through the layers as fit
 
+        # a step runs slots 0 .. the highest busy one (rounded up to a few sizes, one decode graph each): LPT
+        # fills the low slots with the longest utterances, so the tail of a job steps a handful of rows instead
+        # of every slot's (every kernel is row-invariant: the codes do not depend on the row count)
+        sizes = sorted({slots} | {b for b in (1, 2, 4, 8, 16, 24, 32, 40, 48, 56) if b < slots})
+
         fill()
         while any(o >= 0 for o in owner):
             k = min(chunk, max(r for s, r in enumerate(remaining) if owner[s] >= 0))
-            e.step(k, slots=slots)
+            hi = max(s for s in range(slots) if owner[s] >= 0) + 1 if e.batch_shrink else slots
+            e.step(k, slots=next(b for b in sizes if b >= hi))
             e.stream.synchronize()
             e.check_errors()
             act = e.st["active"].cpu()
