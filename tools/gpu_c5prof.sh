@@ -1,8 +1,8 @@
-# C3 sample under rocprofv3 for both many-row GEMM options: per-kernel time
+#!/bin/bash
+# C5-shaped job (8 slots, 430-frame prefix, N new frames) under rocprofv3: per-kernel time
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
 export TMPDIR=/tmp
-for v in 1 2; do
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c3prof$v -o c3 -- python3 -u tools/bench_batch.py "{\"opt_gemm_rows\": $v}" > gpurun_out/c3prof$v.log 2>&1 || exit $?
-find gpurun_out/c3prof$v -name "*kernel_trace*" -delete
-done
+N=${1:-2000}
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o c5 -- python3 -u tools/bench_c5.py $N > gpurun_out/c5prof.log 2>&1 || exit 3
+find gpurun_out/c5prof -name "*kernel_trace*" -delete
