@@ -359,10 +359,13 @@ int zmi_version(void);
  *          later weight slots during the attention phase.
  *   ZMI_OPT_ENG_DELAY (default 0): ns the non-attention workgroups' weight loaders wait at launch start.
  *   ZMI_OPT_ENG_START (default 1): how zmi_ffn_engine's rings start: 0 = every slot at once, 1 = the out_proj slot
- *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest. */
+ *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
+ *   ZMI_OPT_DAC_WIDE (default 1): DAC convs on 256-row time tiles (512-thread workgroups) when the output has at
+ *          least ZMI_OPT_DAC_WIDE_MIN (default 256) 256-row x 32-channel units; 0 = always 128-row tiles, 2 = always
+ *          256. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
-       ZMI_OPT_COUNT = 10 };
+       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_COUNT = 12 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

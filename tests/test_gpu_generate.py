@@ -265,3 +265,30 @@ def test_dac_decode_c5_length_windows_bit_identical():
         a = 0 if lo == 0 else M
         b = hi - lo if hi == T else hi - lo - M
         assert torch.equal(win[..., a * HOP:b * HOP], full[..., (lo + a) * HOP:(lo + b) * HOP]), (lo, hi)
+
+
+@pytest.mark.parametrize("frames", [97, 861])
+def test_dac_wide_time_tiles_bit_identical(frames):
+    """The DAC convs on 256-row time tiles (512-thread workgroups, ZMI_OPT_DAC_WIDE = 2), on 128-row tiles (0) and
+    the default per-conv choice (1) give the same bits, decode and the encoder's latents: a conv output's K order and MFMA
+    chain do not depend on the tile."""
+    from zonos_vibes_amd import _lib
+    from zonos_vibes_amd.autoencoder import DACAutoencoder
+    from tests.helpers import synthetic_wav
+    ae = DACAutoencoder(DEV)
+    codes = torch.randint(0, 1024, (1, 9, frames), generator=torch.Generator().manual_seed(frames)).to(DEV)
+    wav_in = synthetic_wav(1, frames * 512, seed=3).to(DEV)
+    lib = _lib.lib()
+    old = lib.zmi_get_option(_lib.OPT_DAC_WIDE)
+    outs = {}
+    try:
+        for wide in (0, 2, 1):
+            _lib.check(lib.zmi_set_option(_lib.OPT_DAC_WIDE, wide))
+            lat = torch.empty(frames, 1024, dtype=torch.float32, device=DEV)
+            ae.encode_latents(wav_in[0, 0].contiguous(), lat)
+            outs[wide] = (ae.decode(codes).cpu(), lat.cpu())
+    finally:
+        lib.zmi_set_option(_lib.OPT_DAC_WIDE, old)
+    for wide in (2, 1):
+        assert torch.equal(outs[wide][0], outs[0][0]), wide
+        assert torch.equal(outs[wide][1], outs[0][1]), wide

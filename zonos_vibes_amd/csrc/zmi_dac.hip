@@ -72,12 +72,17 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
-constexpr int HALO_PIECES = 12;  // the halo K order's activation tile: up to 192 rows = BN + 64 rows of taps
+constexpr int HALO_TAPS_ROWS = 64;  // the halo K order's activation tile: BN + up to 64 rows of taps
 
-template <int WM, int WN, int NS, bool HALO>
-__global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
+// NWN waves along the time tile (2: 256 threads, BN = 128 rows; 4: 512 threads, BN = 256 rows), 2 along the
+// channels: the wide tile issues each weight tile once per 256 output rows (twice the MFMAs per A piece and
+// per barrier). Every output's K order and MFMA chain are the tile's own, so both give the same bits.
+template <int WM, int WN, int NS, bool HALO, int NWN>
+__global__ __launch_bounds__(128 * NWN) void conv_kernel(const ConvArgs a) {
+  constexpr int NW = 2 * NWN, NT = 64 * NW;
+  constexpr int HALO_PIECES = (16 * WN * NWN + HALO_TAPS_ROWS) / 16;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave - wm * NWN;
   const int kq = (lane >> 4) * 8, lr = lane & 15;
 
   f32x4_t acc[WM][WN];
@@ -97,15 +102,15 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   //   (BN + (taps - 1) |tap_step| rows, the halo) are copied once into one of two halo buffers and each
   //   tap reads its fragments at its row offset, so a step streams only its A tile (8 KB at BM = 128,
   //   against 16 KB with the B tile): the next channel step's halo is issued at this one's first tap.
-  constexpr int BM = 32 * WM, BN = 32 * WN;
+  constexpr int BM = 32 * WM, BN = 16 * WN * NWN;
   constexpr int NPA = BM / 16, NP = (BM + BN) / 16;  // 1 KiB pieces per step
   constexpr int STAGE = HALO ? BM * 64 : (BM + BN) * 64, NSA = HALO ? 2 : NS;
   constexpr int HBUF = HALO ? HALO_PIECES * 1024 : 0;
-  constexpr int TP = BM + 4, TILE_BYTES = (BN / 2) * TP * 4;
+  constexpr int TP = BM + 4, TILE_BYTES = (BN / NWN) * TP * 4;
   constexpr int RING = NSA * STAGE + 2 * HBUF;
   constexpr int LDS_BYTES = RING > TILE_BYTES ? RING : TILE_BYTES;
   __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];
-  float(&tile)[BN / 2][TP] = *reinterpret_cast<float(*)[BN / 2][TP]>(lds_raw);
+  float(&tile)[BN / NWN][TP] = *reinterpret_cast<float(*)[BN / NWN][TP]>(lds_raw);
   const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
   const int rho = blockIdx.z;
   const f16_t* const wts = a.w + (size_t)rho * a.w_phase;
@@ -142,8 +147,8 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
       const int cs = st_ / a.taps, tap_ = st_ - cs * a.taps;
       const int ci_ = cs * 32 + pchunk * 8;
 #pragma unroll
-      for (int k = 0; k < (NPA + 3) / 4; ++k) {
-        const int p = wave + 4 * k;
+      for (int k = 0; k < (NPA + NW - 1) / NW; ++k) {
+        const int p = wave + NW * k;
         if (p < NPA)
           glds16(wts + ((size_t)tap_ * a.c_out + co_blk + 16 * p + prow) * a.c_in + ci_,
                  abuf + (st_ & 1) * STAGE + p * 1024);
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     };
     auto issue_halo = [&](int cs) {
       const int ci_ = cs * 32 + pchunk * 8;
-      for (int p = wave; p < nbp; p += 4) {
+      for (int p = wave; p < nbp; p += NW) {
         const int tin = q_blk + omin + 16 * p + prow;
         const bool ok = tin >= 0 && tin < a.t_in;
         glds16(ok ? (const void*)(a.x + (size_t)tin * a.c_in + ci_) : (const void*)&g_conv_zero[lane & 3],
@@ -177,13 +182,13 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
       }
     }
   } else {
-    const int npw = (NP - wave + 3) / 4;  // this wave's pieces per step: p = wave, wave + 4, ...
+    const int npw = (NP - wave + NW - 1) / NW;  // this wave's pieces per step: p = wave, wave + NW, ...
     auto issue = [&](int st_) {
       const int tap_ = st_ / nci, ci_ = (st_ - tap_ * nci) * 32 + pchunk * 8;
       char* stg = lds_raw + (st_ % NS) * STAGE;
 #pragma unroll
-      for (int k = 0; k < (NP + 3) / 4; ++k) {
-        const int p = wave + 4 * k;
+      for (int k = 0; k < (NP + NW - 1) / NW; ++k) {
+        const int p = wave + NW * k;
         if (p < NP) {
           const void* src;
           if (p < NPA) {
@@ -214,14 +219,14 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
   }
   __syncthreads();  // every wave's last fragment reads are done before the ring is reused as the output tile
   const int tid = threadIdx.x;
-  // epilogue, in two halves of the time tile (the waves with wn == half own it): the accumulators go
+  // epilogue, in NWN parts of the time tile (the waves with wn == half own one): the accumulators go
   // through LDS as an fp32 [t][co] tile, then every thread finishes 8 consecutive channels of one
   // time row, so the skip loads and the raw / snake / f32 stores are whole 16-32 B per lane and
   // each row's BM channels are written contiguously.
-  static_assert(WN == 4, "epilogue halves assume 2 x 64 time rows");
-  constexpr int CPR8 = BM / 8, ROWS = BN / 2;
+  static_assert(WN == 4, "epilogue parts assume 64 time rows each");
+  constexpr int CPR8 = BM / 8, ROWS = BN / NWN;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < NWN; ++half) {
     if (wn == half) {
 #pragma unroll
       for (int i = 0; i < WM; ++i)
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
           *reinterpret_cast<f32x4_t*>(&tile[j * 16 + lr][am + i * 16 + kq / 2]) = acc[i][j];
     }
     __syncthreads();
-    for (int e = tid; e < ROWS * CPR8; e += 256) {
+    for (int e = tid; e < ROWS * CPR8; e += NT) {
       const int row = e / CPR8, c8 = e - row * CPR8;
       const int q = q_blk + half * ROWS + row;
       if (q < a.n_out) {
@@ -454,10 +459,11 @@ extern "C" int zmi_dac_from_codes(const int64_t* codes, int T, const float* code
 // Tile height: the largest BM = 32 WM (WM in 4, 3, 2, 1, dividing c_out) whose grid still gives every CU
 // about two workgroups; the early, few-frame stages (conv1 and block 0 at 861 frames: 84-336 workgroups at
 // BM = 128) are latency-bound per workgroup, so more, shorter tiles finish sooner there.
-static int launch_conv(const ConvArgs& a, hipStream_t s) {
-  constexpr int WN = 4, BN = 32 * WN;
+template <int NWN>
+static int launch_conv_t(const ConvArgs& a, hipStream_t s) {
+  constexpr int WN = 4, BN = 16 * WN * NWN, NT = 128 * NWN;
   const unsigned nq = (unsigned)((a.n_out + BN - 1) / BN), nz = (unsigned)a.nphase;
-  const int want = 256;
+  const int want = 256 / (NWN / 2);
   int wm = 0;
   for (int c : {4, 3, 2, 1})
     if (a.c_out % (32 * c) == 0) {
@@ -471,11 +477,11 @@ static int launch_conv(const ConvArgs& a, hipStream_t s) {
   const int span = (a.taps - 1) * abs(a.tap_step);
   // the halo K order wherever the taps' rows fit its buffer (every DAC conv: dilation <= 9, span <= 54);
   // measured 3.7 -> 3.15 ms DAC decode, 2.11 -> 1.83 ms encode at 861 frames against the tap-major order
-  const bool halo = BN + span <= HALO_PIECES * 16;
-#define ZMI_CONV_L(wm_)                                                                     \
-  do {                                                                                      \
-    if (halo) hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, true>), grid, dim3(256), 0, s, a); \
-    else hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, false>), grid, dim3(256), 0, s, a);     \
+  const bool halo = span <= HALO_TAPS_ROWS;
+#define ZMI_CONV_L(wm_)                                                                               \
+  do {                                                                                                \
+    if (halo) hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, true, NWN>), grid, dim3(NT), 0, s, a);      \
+    else hipLaunchKernelGGL((conv_kernel<wm_, WN, 2, false, NWN>), grid, dim3(NT), 0, s, a);          \
   } while (0)
   switch (wm) {
     case 4: ZMI_CONV_L(4); break;
@@ -485,6 +491,18 @@ static int launch_conv(const ConvArgs& a, hipStream_t s) {
   }
 #undef ZMI_CONV_L
   return 0;
+}
+
+// Tile height: the largest BM = 32 WM (WM in 4, 3, 2, 1, dividing c_out) whose grid still gives every CU
+// about two workgroups; the early, few-frame stages (conv1 and block 0 at 861 frames: 84-336 workgroups at
+// BM = 128) are latency-bound per workgroup, so more, shorter tiles finish sooner there. Time tile: 256 rows
+// (512 threads) where ZMI_OPT_DAC_WIDE allows it and the output has at least that many rows per CU-pair of
+// workgroups, else 128 (256 threads).
+static int launch_conv(const ConvArgs& a, hipStream_t s) {
+  const int wide = zmi_option(ZMI_OPT_DAC_WIDE);
+  if (wide == 2 || (wide == 1 && (long)a.n_out * a.nphase * (a.c_out / 32) >= (long)zmi_option(ZMI_OPT_DAC_WIDE_MIN) * 256))
+    return launch_conv_t<4>(a, s);
+  return launch_conv_t<2>(a, s);
 }
 
 extern "C" int zmi_dac_conv(const void* x, int t_in, int c_in, const void* w, const float* bias, int c_out, int taps,
