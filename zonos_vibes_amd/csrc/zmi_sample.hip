@@ -385,7 +385,10 @@ __global__ __launch_bounds__(64 * ZMI_NCB) void sample_greedy_kernel(const Sampl
   constexpr int PP = (NP + 63) / 64;      // pairs per lane
   const int s = a.slot_begin + blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, k = t >> 6;
-  if (!a.sl.active[s]) return;
+  // no exit before the argmax: a branch on `active` up here would let the compiler sink every load below
+  // behind that round trip (sampler 8.25 -> 8.09 us, profiles/r04_sampler_hoist_ab.jsonl). An inactive slot's
+  // state is valid (its last utterance's), the penalty indices are clamped, and it leaves before any write.
+  const int act0 = a.sl.active[s];
   const int lrow = 2 * blockIdx.x;
   const float2* lc = reinterpret_cast<const float2*>(a.logits + ((size_t)lrow * ZMI_NCB + k) * NV);
   const float2* lu = reinterpret_cast<const float2*>(a.logits + ((size_t)(lrow + 1) * ZMI_NCB + k) * NV);
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(64 * ZMI_NCB) void sample_greedy_kernel(const Sampl
     const int win_lo = P.rep_window > 0 ? max(0, o - P.rep_window) : min(o, -P.rep_window);
     for (int v = lane; v < NV; v += 64) cnt[k][v] = 0;
     __syncthreads();
-    for (int i = win_lo + lane; i < o; i += 64) atomicAdd(&cnt[k][min(dl[i], NV - 1)], 1);
+    for (int i = win_lo + lane; i < min(o, a.sl.tcap); i += 64) atomicAdd(&cnt[k][min(max(dl[i], 0), NV - 1)], 1);
     __syncthreads();
   }
   float bv = -INFINITY;
@@ -441,6 +444,7 @@ __global__ __launch_bounds__(64 * ZMI_NCB) void sample_greedy_kernel(const Sampl
       bi = oi;
     }
   }
+  if (!act0) return;  // slot-uniform; nothing written before it
   if (lane == 0) {
     tokv[k] = bi;
     a.next[(size_t)s * ZMI_NCB + k] = bi;
