@@ -84,21 +84,37 @@ __device__ int block_argmax(float v, int idx, float* redv, int* redi) {
   return bi;
 }
 
+// the keys are distinct (the index is in the low word), so any correct sort gives the same array; each thread
+// owns SORTN / 512 compare-exchange pairs per stage (pair p: i = p with a zero bit inserted at j, partner i + j)
 __device__ void bitonic_desc(uint64_t* keys) {
   for (int k = 2; k <= SORTN; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < SORTN; i += 256) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t x = keys[i], y = keys[ixj];
-          const bool first_desc = (i & k) == 0;
-          if (first_desc ? (x < y) : (x > y)) {
-            keys[i] = y;
-            keys[ixj] = x;
-          }
+      constexpr int NQ = SORTN / 512;
+      int ii[NQ];
+      uint64_t xv[NQ], yv[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {  // every pair's two keys in flight before the first compare
+        const int p = threadIdx.x + 256 * q;
+        ii[q] = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+        xv[q] = keys[ii[q]];
+        yv[q] = keys[ii[q] + j];
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const bool first_desc = (ii[q] & k) == 0;
+        if (first_desc ? (xv[q] < yv[q]) : (xv[q] > yv[q])) {
+          keys[ii[q]] = yv[q];
+          keys[ii[q] + j] = xv[q];
         }
       }
-      __syncthreads();
+      // stages with j <= 64 touch only the wave's own 128-key blocks (pairs p of one wave span 64 consecutive
+      // p per q): between two such stages the wave's own LDS order suffices (a wave's LDS operations complete
+      // in order), every other edge is a workgroup barrier
+      const int jn = j > 1 ? j >> 1 : k;  // the next stage's distance (k doubles after j = 1)
+      if (j <= 64 && jn <= 64 && !(j == 1 && k == SORTN))
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        __syncthreads();
     }
 }
 
@@ -237,12 +253,17 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
       }
       dscan[t] = run;
       __syncthreads();
-      if (t == 0) {  // exclusive scan of the 256 thread totals, in order
+      if (t == 0) {  // exclusive scan of the 256 thread totals, in order (loads batched ahead of the add chain)
         double acc = 0.0;
-        for (int i = 0; i < 256; ++i) {
-          const double x = dscan[i];
-          dscan[i] = acc;
-          acc += x;
+        for (int i0 = 0; i0 < 256; i0 += 16) {
+          double x[16];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) x[i] = dscan[i0 + i];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            dscan[i0 + i] = acc;
+            acc += x[i];
+          }
         }
       }
       __syncthreads();
