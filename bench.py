@@ -105,7 +105,7 @@ def time_dominant_kernel(model, cond, reps: int = 3):
     return tot / (reps * len(items)), bytes_launch, name
 
 
-# the committed FETCH_SIZE pass of each dominant-kernel candidate (tools/prof_round.sh)
+# the committed FETCH_SIZE pass of each dominant-kernel candidate (tools/gpu.sh round)
 PMC_FILES = {"layer_engine_kernel<0>": "r04_pmc_engine_fetch.json",
              "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": "r04_pmc_fc1_fetch.json"}
 
@@ -131,7 +131,7 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of the dominant kernel from the committed FETCH_SIZE pass of THIS kernel
-    (tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950
+    (tools/gpu.sh round: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950
     correction; a counter pass serialises dispatches, so it is not repeated inside the timed run). None
     when the profile is absent or measured another kernel."""
     name = PMC_FILES.get(kernel)
@@ -658,7 +658,10 @@ def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430, engine_op
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_slots=slots, max_seqlen=LC + prefix + n_new + 9,
                         max_prefill=LC + prefix + 1)
     for k, v in (engine_opts or {}).items():  # A/B knobs (tools/bench_c5.py)
-        setattr(m.engine, k, v)
+        if k.startswith("opt_"):  # library launch knobs: opt_splitk_reduce -> zmi_set_option(OPT_SPLITK_REDUCE)
+            _lib.check(m.engine.lib.zmi_set_option(getattr(_lib, "OPT_" + k[4:].upper()), int(v)), k)
+        else:
+            setattr(m.engine, k, v)
     m.engine._build_plan()
     g = torch.Generator().manual_seed(11)
     conds = [cond_tensor(200 + i, cfg.backbone.d_model, dev) for i in range(slots)]

@@ -238,13 +238,17 @@ def test_hybrid_generate_batch_equals_single():
 
 def test_hybrid_full_dims_generate_and_backbone_plugin():
     """Zonos-v0.1-hybrid dims (46 layers, 2.3 GB bf16): generate() through the hipGraph decode loop, and the
-    BACKBONES['hip'] plugin's forward equals the engine's prefill (same kernels)."""
+    BACKBONES['hip'] plugin's forward over the 40 conditioning rows of both CFG halves equals, bit for bit, the
+    norm_f'd hidden states of the engine's own prefill of the same rows (the prefill carries one more row, the
+    embedded first frame, which causal attention and the Mamba2 scan keep out of the earlier rows)."""
     from zonos_vibes_amd.backbone import BACKBONES
     from zonos_vibes_amd.config import InferenceParams, zonos_v01_hybrid
+    from zonos_vibes_amd.engine import SamplingParams
     from zonos_vibes_amd.model import Zonos
     cfg = zonos_v01_hybrid()
     m = Zonos.synthetic(cfg, DEV, seed=0, zero_eos=True, max_seqlen=256, max_prefill=64)
-    cond = _bf(2, 40, 2048, seed=50).to(DEV)
+    lc = 40
+    cond = _bf(2, lc, 2048, seed=50).to(DEV)
     codes = m.generate(cond, max_new_tokens=64, sampling_params=dict(temperature=0.0), progress_bar=False)
     assert codes.shape == (1, 9, 64) and int(codes.max()) < 1024
     bb = BACKBONES["hip"](cfg.backbone)
@@ -252,7 +256,17 @@ def test_hybrid_full_dims_generate_and_backbone_plugin():
     cache = bb.allocate_inference_cache(2, 64)
     assert len(cache) == 46
     out = bb(cond, InferenceParams(64, 2, key_value_memory_dict=cache))
-    assert out.shape == (2, 40, 2048) and torch.isfinite(out.float()).all()
+    assert out.shape == (2, lc, 2048) and torch.isfinite(out.float()).all()
+    e = m.engine
+    s_len = e.prefill(0, cond, None, 8, SamplingParams(temperature=0.0))
+    assert s_len == lc + 1
+    ref = torch.empty(2 * s_len, 2048, dtype=torch.bfloat16, device=DEV)
+    with torch.cuda.stream(e.stream):
+        e.final_norm_pre(2 * s_len, ref)
+    e.stream.synchronize()
+    e.release(0)
+    assert torch.equal(out[0], ref[:lc])
+    assert torch.equal(out[1], ref[s_len: s_len + lc])
 
 
 def synthetic_weights_gpu(m):

@@ -3,15 +3,20 @@ transformer dims (26 layers), C2 conditioning (Lc = 160), synthetic weights -- t
 own teacher-forced outputs along its 1,125-frame greedy trajectory (tests/golden/full_model_long.safetensors,
 make_golden_full_long.py; reference zonos/model.py:240-307, zonos/backbone/_torch.py:99-152).
 
-The decode steps run at positions 162 .. 1,294 and cross every form switch of the launch plan (the chunk-split
-fused attention to position 1,023, the score-exchange form to 1,279, the separate QKV + chunked attention beyond)
-and the softmax blocks of 512 keys. Criteria (the reference's own thread-count noise at these positions is the
-yardstick, fixture metadata `self_noise`):
-  * every teacher-forced greedy decision whose reference margin exceeds twice that noise is identical;
+The decode steps run at positions 162 .. 1,294 and cross the softmax blocks of 512 keys. The default launch plan
+runs the chunk-split fused attention to position 1,023 and its 24-chunk form beyond (asserted); a second pass with
+attn_forms = ("split", "xs") runs the score-exchange form to 1,279 and the separate QKV + chunked attention beyond
+(asserted), so every decode path keeps reference parity past position 1,023. Criteria (the reference's own
+thread-count noise at these positions is the yardstick, fixture metadata `self_noise`):
+  * every teacher-forced greedy decision whose reference margin exceeds twice that noise ("determined") is
+    identical -- about 30 % of all decisions; the rest are the reference's own near-ties;
+  * over ALL teacher-forced decisions, HIP's raw argmax disagreement rate with the reference is at most 1.25x the
+    reference's own 1-vs-8-thread disagreement rate (20 of 315 recorded decisions);
   * CFG'd logits of the recorded windows (positions 588-596, 1,018-1,028, 1,278-1,292): mean error within 1.5x
     the noise mean, max within 2x the noise max (bf16 ulps of each decision's top score);
   * free-running generate(): the first divergence from the reference trajectory, if any, is at a decision the
     reference leaves undetermined.
+The agreement of decisions whose margin lies between 1x and 2x the noise is reported (not asserted).
 """
 import json
 import os
@@ -54,7 +59,7 @@ def long_fix():
     torch.cuda.empty_cache()
 
 
-def test_full_depth_long_teacher_forced(long_fix):
+def _teacher_forced(long_fix, forms_want, out_name):
     from oracle.zonos_cpu import apply_delay_pattern, repetition_penalty
     from zonos_vibes_amd.engine import SamplingParams
     model, t, meta, cond = long_fix
@@ -94,7 +99,9 @@ def test_full_depth_long_teacher_forced(long_fix):
     # every decision along the reference trajectory (decision i writes frame i + 1 into the codebooks still
     # unknown there, model.py:258-260,296-297)
     floor = 2 * noise["max_ulps"]
-    det = t["margin"] > floor * _ulp(t["top"])
+    margin_ulps = t["margin"] / _ulp(t["top"])
+    det = margin_ulps > floor
+    band = (margin_ulps > noise["max_ulps"]) & ~det  # between 1x and 2x the reference's noise
     got_arg = torch.stack([sc.argmax(-1) for sc in scores])
     init = apply_delay_pattern(torch.full((1, 9, n), -1), 1025)[0]
     agree = torch.ones_like(det)
@@ -105,17 +112,48 @@ def test_full_depth_long_teacher_forced(long_fix):
             used[i, m] = True
             agree[i, m] = bool(got_arg[i, m] == delayed[k, i + 1])
     det = det & used
+    band = band & used
     bad = (det & ~agree).nonzero().tolist()
+    decisions = int(used.sum())
+    raw_dis = decisions - int((agree & used).sum())
+    ref_rate = noise["raw_argmax_disagreements"] / noise["decisions"]
     stats = dict(positions=[lc + 1, lc + n + 8], forms=sorted(forms), window_steps=len(win_logits),
                  mean_err_ulps=float(errs.mean()), max_err_ulps=float(errs.max()), ref_self_noise=noise,
                  within_thread_noise_frac=float((errs <= noise["max_ulps"]).float().mean()),
-                 decisions=int(used.sum()), agree=int((agree & used).sum()), determined=int(det.sum()),
-                 determined_disagreements=len(bad), first_bad=bad[:5])
+                 decisions=decisions, agree=decisions - raw_dis, determined=int(det.sum()),
+                 determined_frac=float(det.sum()) / decisions,
+                 determined_disagreements=len(bad), first_bad=bad[:5],
+                 raw_disagreement_rate=raw_dis / decisions, ref_thread_disagreement_rate=ref_rate,
+                 raw_rate_vs_ref=raw_dis / decisions / ref_rate,
+                 band_1x_2x_noise=dict(decisions=int(band.sum()), agree=int((band & agree).sum())))
     if os.path.isdir("gpurun_out"):
-        json.dump(stats, open("gpurun_out/full_parity_long.json", "w"), indent=1)
+        json.dump(stats, open(f"gpurun_out/{out_name}.json", "w"), indent=1)
+    assert set(forms) == forms_want, stats
     assert stats["determined_disagreements"] == 0, stats
+    assert stats["raw_rate_vs_ref"] <= 1.25, stats
     assert errs.mean() <= 1.5 * noise["mean_ulps"], stats
     assert errs.max() <= 2 * noise["max_ulps"], stats
+
+
+def test_full_depth_long_teacher_forced(long_fix):
+    """The default plan: the chunk-split fused block to position 1,023, its 24-chunk form beyond."""
+    e = long_fix[0].engine
+    assert e.attn_forms == ("split", "split24", "xs")
+    _teacher_forced(long_fix, {"split", "split24"}, "full_parity_long")
+
+
+def test_full_depth_long_teacher_forced_xs_and_separate(long_fix):
+    """The same decisions through the score-exchange fused form (to position 1,279) and the separate QKV GEMV +
+    chunked attention launches beyond (the 24-chunk form off)."""
+    e = long_fix[0].engine
+    saved = e.attn_forms
+    e.attn_forms = ("split", "xs")
+    e._build_plan()
+    try:
+        _teacher_forced(long_fix, {"split", "xs", "none"}, "full_parity_long_xs")
+    finally:
+        e.attn_forms = saved
+        e._build_plan()
 
 
 def test_full_depth_long_greedy_trajectory(long_fix):

@@ -26,11 +26,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pos", type=int, default=591)
     ap.add_argument("--slices", type=int, default=8)
-    ap.add_argument("--form", default="split", help="split (chunk workgroups), self (self-scoring) or xs (score exchange)")
+    ap.add_argument("--form", default="split",
+                    help="split / split24 (chunk workgroups), self (self-scoring) or xs (score exchange)")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=1040, max_prefill=16)
+    m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=max(1040, args.pos + 24),
+                        max_prefill=16)
     e = m.engine
     e.attn_block_slices = e.attn_self_slices = args.slices
     with torch.cuda.stream(e.stream):

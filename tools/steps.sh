@@ -1,10 +1,10 @@
 #!/bin/bash
 # GPU-box runner: each GPU step under its own time limit; stop at the first fault/abort/timeout.
-# Usage: bash tools/gpu_round.sh "<step1>" "<step2>" ...
+# Usage: bash tools/steps.sh "<step1>" "<step2>" ...
 # A step may fail with rc 1 (pytest test failures, python assertion) and the next step still runs,
 # unless its output shows a GPU fault; any other nonzero rc (timeout 124/137, abort 134, segv 139)
 # ends the call.
-mkdir -p gpurun_out
+mkdir -p gpurun_out/keep
 i=0
 for step in "$@"; do
   i=$((i+1))

@@ -119,15 +119,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
     }
     __syncthreads();
     ZMI_ASTAMP(1);
-#ifdef ZMI_ATTN_BCUT  // timing-only build: the finish launch stops once M_j and V^T are in (wrong output)
-    {
-      uint32_t x = 0;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) x ^= vf[dt].x ^ vf[dt].w;
-      if (x == 0x9e3779b9u || t == 0) a.out[(size_t)qi * a.ldo + kh * G * HD + (t & 127)] = (bf16_t)(x & 0xffff);
-      return;
-    }
-#endif
   } else {
   if constexpr (G == 4) {
     if (wave == 0) zmi_gemv::dma_piece(a.q + (size_t)qi * a.ldq + kh * G * HD + lane * 8, qs);
@@ -208,11 +199,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   // ---- running maximum M_j = max over the chunks of blocks 0..j: {value, tag} granule exchange ----
   uint64_t* gu = a.gran + (size_t)unit * a.nch * G;
   if (MODE == 0 && nc > 1 && t < G) st_wt64(gu + c * G + t, pack_f2(mj[t], 1.0f));  // {value, tag 1.0f}: untorn granule
-#ifdef ZMI_ATTN_NOEXCH  // timing experiment only: wrong numerics
-  if (false) {
-#else
   if (MODE == 0 && dep > 1) {
-#endif
     float m = -INFINITY;
     for (int e = t; e < dep * G; e += NT) {  // e = chunk * G + head
       if (e / G == c) {
@@ -673,6 +660,13 @@ hipError_t launch_chunked(const AttnArgs& a, unsigned blocks, int variant, hipSt
 
 extern "C" int zmi_attention_max_keys_whole(void) { return DS_KEYS; }
 
+// The kernel zmi_attention_pf launches for `variant` (0 = the library's choice, resolved here): the launcher
+// calls this too, so a caller (tests/test_gpu_scale.py) can assert which form a decode step's plan takes.
+extern "C" int zmi_attention_pick(int n_query, int hkv, int variant) {
+  if (variant != 0) return variant;
+  return (int64_t)n_query * hkv >= 32 ? 5 : 1;
+}
+
 extern "C" int zmi_attention(const void* q, int ldq, const void* k_cache, const void* v_cache, const int* q_kv_row,
                              const int* q_pos, int n_query, int hq, int hkv, int hd, int smax, int max_pos, void* out,
                              int ldo, float* part_o, float* part_lm, void* work, void* stream) {
@@ -740,7 +734,7 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
   // 16 rows at the engine's launch shape (max_pos = the C5 KV capacity 5783) x 1000 / 1600 / 2600 / 5000 keys:
   // 17.5 / 19.9 / 30.3 / 44.8 us against 21.4 / 26.6 / 32.8 / 52.6 chunked; 8 rows x 3200 20.4 against 25.3;
   // 128 rows x 1000 equal; 2 rows x 3200 18.1 against 15.6 (profiles/r04_attn_block_form.jsonl).
-  if (variant == 0) variant = (int64_t)n_query * hkv >= 32 ? 5 : 1;
+  variant = zmi_attention_pick(n_query, hkv, variant);
   if (variant < 1 || (variant > 3 && variant != 5)) {
     a.stamps = nullptr;  // the diagnostic stamp area is laid out for the chunked grid
     if (max_pos >= DS_KEYS) return zmi_fail_msg("attention: the whole-query variant covers positions < 1280");

@@ -85,16 +85,23 @@ __device__ int block_argmax(float v, int idx, float* redv, int* redi) {
 }
 
 // the keys are distinct (the index is in the low word), so any correct sort gives the same array; each thread
-// owns SORTN / 512 compare-exchange pairs per stage (pair p: i = p with a zero bit inserted at j, partner i + j)
+// owns SORTN / 512 compare-exchange pairs per stage (pair p: i = p with a zero bit inserted at j, partner i + j).
+// Requires exactly 256 threads (pair p = threadIdx.x + 256 q) and 64-lane waves (one wave's 64 consecutive pairs
+// cover one 128-key block: the barrier-free stages below rely on it); the launchers use 256-thread workgroups.
+constexpr int SORT_THREADS = 256;
+static_assert(SORTN % (2 * SORT_THREADS) == 0, "whole compare-exchange pairs per thread");
 __device__ void bitonic_desc(uint64_t* keys) {
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "bitonic_desc's barrier-free stages assume 64-lane waves"
+#endif
   for (int k = 2; k <= SORTN; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
-      constexpr int NQ = SORTN / 512;
+      constexpr int NQ = SORTN / (2 * SORT_THREADS);
       int ii[NQ];
       uint64_t xv[NQ], yv[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {  // every pair's two keys in flight before the first compare
-        const int p = threadIdx.x + 256 * q;
+        const int p = threadIdx.x + SORT_THREADS * q;
         ii[q] = ((p & ~(j - 1)) << 1) | (p & (j - 1));
         xv[q] = keys[ii[q]];
         yv[q] = keys[ii[q] + j];
@@ -156,7 +163,7 @@ __device__ void softmax_inplace(float* x, float* red) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
+__global__ __launch_bounds__(SORT_THREADS) void sample_kernel(const SampleArgs a) {
   __shared__ float probs[NV + 2];
   __shared__ int cnt[NV];
   __shared__ uint64_t keys[SORTN];
@@ -646,7 +653,7 @@ extern "C" int zmi_sample_logits(const float* logits, const int* generated, int 
   a.gen = generated;
   a.gen_len = generated ? gen_len : 0;
   a.params1 = params;
-  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, batch), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, batch), dim3(SORT_THREADS), 0, (hipStream_t)stream, a);
   ZMI_CHECK(hipGetLastError());
   return 0;
 }
@@ -671,7 +678,7 @@ extern "C" int zmi_sample_step(const ZmiSlots* slots, const float* logits_rows, 
   a.x = (bf16_t*)x;
   a.row_kv = row_kv;
   a.row_pos = row_pos;
-  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, slot_count), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(sample_kernel, dim3(ZMI_NCB, slot_count), dim3(SORT_THREADS), 0, (hipStream_t)stream, a);
   ZMI_CHECK(hipGetLastError());
   return 0;
 }

@@ -27,6 +27,7 @@ from .config import EMB_VOCAB, HEAD_VOCAB, N_CODEBOOKS, ROPE_TABLE_LEN, ZonosCon
 HEADS_N = N_CODEBOOKS * 1026            # 9 heads x (1025 + 1 pad row), model.py:37 + utils.py:12-27
 HEADS_N_PAD = (HEADS_N + 15) // 16 * 16
 PREFILL_BATCH_ROWS = 2048  # rows of one batched prefill pass (prefill_many): 6 C2-sized utterances (2 x 161)
+BLK_ROWS_MAX = 16  # rows zmi_attn_block takes (one MFMA row tile, include/zonos_hip.h)
 
 
 def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
@@ -226,15 +227,21 @@ class HipEngine:
             nf = self.lib.zmi_attention_partial_floats(nq, self.H, self.Hkv, self.hd, self.smax - 1)
             self.attn_o = z(nf, dt=torch.float32)        # attention chunk partials (zmi_attn_merge.h)
             self.attn_lm = z(nf // self.hd * 2, dt=torch.float32)
-            # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer; a row's
-            # areas are zeroed when it starts an utterance (prefill), and its error word
-            self.blk_gran = z(self.n_kv, R, self.lib.zmi_attn_block_gran_words(1, self.Hkv), dt=torch.int64)
+            # zmi_attn_block hand-off granules {value, tag = position + 1}, one area per layer and row; a row's
+            # areas are zeroed when it starts an utterance (prefill), and its error word. Only the first
+            # BLK_ROWS_MAX rows can run the fused block (one 16-row tile), so only they get an area: at 128 rows
+            # (C3's 64 slots) 26 x 16 areas of 104 KB instead of 26 x 128
+            self.blk_rows = min(R, BLK_ROWS_MAX)
+            self.blk_gran = z(self.n_kv, self.blk_rows, self.lib.zmi_attn_block_gran_words(1, self.Hkv),
+                              dt=torch.int64)
             self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block,
             # [4] attn_ffn_block, [5] ffn_engine, [6] layer_engine
             # hand-off granules of the diagnostic forms (zonos_diag.h), allocated on first use (_diag_alloc)
             self.eng_gran = self.lay_gran = self.ffn_gran = self.attn_gran = None
-            # zmi_gemv_splitk's fp32 segment sums (fc2 over many rows: decode and prefill)
+            # zmi_gemv_splitk's fp32 segment sums (fc2 / out_proj over many rows: decode and prefill), after its
+            # in-launch reduce counters (zeroed here, re-armed by every launch)
             self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
+            self.splitk_hdr, self.splitk_err = self.lib.zmi_gemv_splitk_layout(0), self.lib.zmi_gemv_splitk_layout(1)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -338,7 +345,8 @@ class HipEngine:
     def _use_splitk(self, a, epi) -> bool:
         lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows}.get(a.K, 0)
         return (lo > 0 and a.M >= lo and epi == _lib.EPI_RESIDUAL and not a.ln_w and a.pro == _lib.PRO_AUTO
-                and a.N % 64 == 0 and a.n_valid == a.N and a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
+                and a.N % 64 == 0 and a.n_valid == a.N
+                and self.splitk_hdr + a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
 
     def _build_plan(self):
         """Invalidate the per-row-count decode plans and graphs (new weights or buffers)."""
@@ -412,7 +420,8 @@ class HipEngine:
         out = []
         if self._use_layer_engine(rows):
             out.append(("engine", self.dlib.zmi_layer_engine_max_pos()))
-        if self.attn_block and rows <= self.attn_block_rows and self.d == 2048 and self.H == 4 * self.Hkv:
+        if (self.attn_block and rows <= min(self.attn_block_rows, self.blk_rows) and self.d == 2048
+                and self.H == 4 * self.Hkv):
             for f in self.attn_forms:
                 if f not in ("xs", "split24") or rows <= self.attn_xs_rows:
                     out.append((f, self.lib.zmi_attn_block_max_pos(self._block_slices(f))))
@@ -586,12 +595,16 @@ class HipEngine:
         its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
         attn = int(self.attn_work[:4].view(torch.int32).item())
         blk, mamba, _, ffn, af, eng, leng = (int(v) for v in self.blk_err[:7].tolist())
-        if attn or blk or mamba or ffn or af or eng or leng:
+        sk = int(self.splitk_part[self.splitk_err:self.splitk_err + 1].view(torch.int32).item())
+        if attn or blk or mamba or ffn or af or eng or leng or sk:
             with torch.cuda.stream(self.stream):  # ordered with the engine's launches
                 self.attn_work[:4].zero_()
                 self.blk_err[:2].zero_()
                 self.blk_err[3:7].zero_()
+                self.splitk_part[self.splitk_err:self.splitk_err + 1].zero_()
             self.stream.synchronize()
+        if sk:
+            raise RuntimeError("gemv_splitk: an in-launch reduce workgroup timed out waiting (results are invalid)")
         if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
         if blk:
@@ -803,7 +816,8 @@ class HipEngine:
 
     def _reset_granules(self, slot: int):
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
-        self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
+        if 2 * slot < self.blk_rows:
+            self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
         if self.eng_gran is not None:  # the diagnostic forms' areas, once allocated
             self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
             self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
