@@ -658,7 +658,7 @@ def time_c5(dev, slots: int = 8, n_new: int = 5168, prefix: int = 430, engine_op
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_slots=slots, max_seqlen=LC + prefix + n_new + 9,
                         max_prefill=LC + prefix + 1)
     for k, v in (engine_opts or {}).items():  # A/B knobs (tools/bench_c5.py)
-        if k.startswith("opt_"):  # library launch knobs: opt_splitk_reduce -> zmi_set_option(OPT_SPLITK_REDUCE)
+        if k.startswith("opt_"):  # library launch knobs: opt_gemm_rows -> zmi_set_option(OPT_GEMM_ROWS)
             _lib.check(m.engine.lib.zmi_set_option(getattr(_lib, "OPT_" + k[4:].upper()), int(v)), k)
         else:
             setattr(m.engine, k, v)

@@ -72,20 +72,15 @@ int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
 /* Many-row fc2 (K = 8192) or out_proj (K = 2048), EPI_RESIDUAL, plain (reference _torch.py:100-101,141,152): a
  * split-K GEMM (one workgroup per 64-column block and K segment -- 8 x 1024 / 4 x 512, the GEMV's wave split --,
- * fp32 segment sums in `part`, then a reduce adding the segments in K order + the residual epilogue: up to 32 rows
- * in the same launch, by reduce workgroups that wait for every GEMM workgroup; beyond, a second launch).
- * Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment MFMA chains and segment order); reads the
- * activation rows once per column block instead of once per column group. part: zmi_gemv_splitk_floats(M, N)
- * floats, ZEROED before the first launch (its first zmi_gemv_splitk_layout(0) floats hold the in-launch reduce's
- * counters, which every launch re-arms; word zmi_gemv_splitk_layout(1), as int, is an error flag: nonzero if a
- * reduce workgroup gave up waiting). */
+ * fp32 segment sums in `part`, then a reduce launch adding the segments in K order + the residual epilogue). Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment MFMA chains and segment
+ * order); reads the activation rows once per column block instead of once per column group. part:
+ * zmi_gemv_splitk_floats(M, N) floats. */
 int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream);
 /* The same with ln_w != NULL (N = 2048): the reduce also writes LayerNorm(new row; ln_w, ln_b, eps) to xn [M][ldxn],
  * bit-identical to zmi_layernorm_rows of the new rows, so the next op's LayerNorm pre-pass is not launched. */
 int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, const void* ln_w,
                        const void* ln_b, float eps, void* xn, int ldxn, void* stream);
 int64_t zmi_gemv_splitk_floats(int M, int N);
-int zmi_gemv_splitk_layout(int which);
 /* out[r] = LayerNorm(x[r]) bf16, r < m (nn.LayerNorm, _torch.py:62: norm_f for the backbone plugin),
  * with the GEMV LayerNorm prologue's arithmetic; k in {512, 1024, 2048, 4096}. */
 int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps, void* out,
@@ -370,14 +365,10 @@ int zmi_version(void);
  *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
  *   ZMI_OPT_DAC_WIDE (default 1): DAC convs on 256-row time tiles (512-thread workgroups) when the output has at
  *          least ZMI_OPT_DAC_WIDE_MIN (default 256) 256-row x 32-channel units; 0 = always 128-row tiles, 2 = always
- *          256.
- *   ZMI_OPT_SPLITK_REDUCE (default 2): the reduce of zmi_gemv_splitk(_ln): 0 = a second launch, one 256-thread
- *          workgroup per row (LN) or per 256 elements; 1 = up to 32 rows in the GEMM's own launch (reduce workgroups
- *          appended to its grid wait for every GEMM workgroup), else as 2; 2 = a second launch, one 512-thread
- *          workgroup per row (N = 2048), else as 0. */
+ *          256. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
-       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_SPLITK_REDUCE = 12, ZMI_OPT_COUNT = 13 };
+       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_COUNT = 12 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

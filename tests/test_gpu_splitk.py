@@ -1,11 +1,8 @@
 """The split-K fc2 / out_proj GEMM (zmi_gemv_splitk: one workgroup per 64-column block and K segment -- 8 x 1024
-for K = 8192, 4 x 512 for K = 2048 --, fp32 segment sums, a reduce adding them in K order + the residual
+for K = 8192, 4 x 512 for K = 2048 --, fp32 segment sums, a reduce launch adding them in K order + the residual
 epilogue) against zmi_gemv_launch's GEMV for the same EPI_RESIDUAL op: bit-identical for row counts on and off
 the 16-row tile and across the GEMV's own launch forms at those counts (a row's result may not depend on the
-batch it is computed in). Every reduce form (ZMI_OPT_SPLITK_REDUCE): a second launch with one 512-thread workgroup
-per row (2, the default) or 256-thread workgroups (0), and in the GEMM's own launch (1: reduce workgroups waiting
-on the GEMM workgroups' arrival counters, up to 32 rows; re-armed by every launch, so the same buffer is launched
-three times)."""
+batch it is computed in)."""
 import ctypes
 
 import pytest
@@ -18,33 +15,9 @@ pytestmark = pytest.mark.gpu
 D, F = 2048, 8192
 
 
-def _part(L, M):
-    nf = L.lib().zmi_gemv_splitk_floats(M, D)
-    part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
-    part[: L.lib().zmi_gemv_splitk_layout(0)] = 0  # the in-launch reduce's counters (zeroed once)
-    return part, nf
-
-
-@pytest.fixture(params=[2, 1, 0], ids=["row_reduce_launch", "in_launch_reduce", "reduce_launch"])
-def fused(request):
-    L = _lib()
-    old = L.lib().zmi_get_option(L.OPT_SPLITK_REDUCE)
-    L.check(L.lib().zmi_set_option(L.OPT_SPLITK_REDUCE, request.param))
-    yield request.param
-    L.check(L.lib().zmi_set_option(L.OPT_SPLITK_REDUCE, old))
-
-
-def _check_hdr(part):
-    torch.cuda.synchronize()
-    lib = _lib().lib()
-    hdr = part[: lib.zmi_gemv_splitk_layout(0)].view(torch.int32).cpu()
-    assert int(hdr[lib.zmi_gemv_splitk_layout(1)]) == 0, "a reduce workgroup gave up waiting"
-    assert int(hdr.abs().sum()) == 0, hdr.nonzero().flatten().tolist()  # every counter re-armed for the next launch
-
-
 @pytest.mark.parametrize("K", [F, D])
-@pytest.mark.parametrize("M", [1, 16, 17, 32, 64, 65, 128, 322])
-def test_splitk_bit_identical_to_gemv(M, K, fused):
+@pytest.mark.parametrize("M", [1, 16, 17, 64, 65, 128, 322])
+def test_splitk_bit_identical_to_gemv(M, K):
     L = _lib()
     W = rnd(D, K, scale=0.03, seed=70)
     Wp = pack(W)[0]
@@ -60,18 +33,18 @@ def test_splitk_bit_identical_to_gemv(M, K, fused):
     ref = x0.clone()
     a = args(ref)
     L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), L.EPI_RESIDUAL, stream_ptr()))
-    part, nf = _part(L, M)
-    for _ in range(3):
-        got = x0.clone()
-        a = args(got)
-        L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, stream_ptr()), "splitk")
-        _check_hdr(part)
-        assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
+    got = x0.clone()
+    nf = L.lib().zmi_gemv_splitk_floats(M, D)
+    part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
+    a = args(got)
+    L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, stream_ptr()), "splitk")
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
 
 
 @pytest.mark.parametrize("K", [F, D])
-@pytest.mark.parametrize("M", [1, 16, 31, 32, 33, 128])
-def test_splitk_fused_layernorm_bit_identical(M, K, fused):
+@pytest.mark.parametrize("M", [16, 33, 128])
+def test_splitk_fused_layernorm_bit_identical(M, K):
     """zmi_gemv_splitk_ln: the reduce also writes LayerNorm(new rows) -- equal to the GEMV followed by
     zmi_layernorm_rows (the next op's pre-pass it replaces)."""
     L = _lib()
@@ -93,16 +66,16 @@ def test_splitk_fused_layernorm_bit_identical(M, K, fused):
     ref_n = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
     L.check(L.lib().zmi_layernorm_rows(ref.data_ptr(), D, M, D, lw.data_ptr(), lb.data_ptr(), 1e-5, ref_n.data_ptr(), D,
                                        stream_ptr()))
-    part, nf = _part(L, M)
-    for _ in range(3):
-        got = x0.clone()
-        got_n = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
-        a = args(got)
-        L.check(L.lib().zmi_gemv_splitk_ln(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, lw.data_ptr(),
-                                           lb.data_ptr(), 1e-5, got_n.data_ptr(), D, stream_ptr()), "splitk_ln")
-        _check_hdr(part)
-        assert torch.equal(got, ref)
-        assert torch.equal(got_n, ref_n), (got_n != ref_n).nonzero()[:4].tolist()
+    got = x0.clone()
+    got_n = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    nf = L.lib().zmi_gemv_splitk_floats(M, D)
+    part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
+    a = args(got)
+    L.check(L.lib().zmi_gemv_splitk_ln(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, lw.data_ptr(), lb.data_ptr(),
+                                       1e-5, got_n.data_ptr(), D, stream_ptr()), "splitk_ln")
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(got_n, ref_n), (got_n != ref_n).nonzero()[:4].tolist()
 
 
 def test_engine_splitk_and_attention_prefetch_bit_identical():

@@ -29,7 +29,6 @@ OPT_ENG_PF = 8
 OPT_ENG_DELAY = 9
 OPT_DAC_WIDE = 10
 OPT_DAC_WIDE_MIN = 11
-OPT_SPLITK_REDUCE = 12
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
@@ -134,7 +133,6 @@ _SIGS = {
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
-    "zmi_gemv_splitk_layout": (c_int, [c_int]),
     "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,
                                    c_void_p, c_int, c_void_p]),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -238,10 +238,8 @@ class HipEngine:
             # [4] attn_ffn_block, [5] ffn_engine, [6] layer_engine
             # hand-off granules of the diagnostic forms (zonos_diag.h), allocated on first use (_diag_alloc)
             self.eng_gran = self.lay_gran = self.ffn_gran = self.attn_gran = None
-            # zmi_gemv_splitk's fp32 segment sums (fc2 / out_proj over many rows: decode and prefill), after its
-            # in-launch reduce counters (zeroed here, re-armed by every launch)
+            # zmi_gemv_splitk's fp32 segment sums (fc2 / out_proj over many rows: decode and prefill)
             self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
-            self.splitk_hdr, self.splitk_err = self.lib.zmi_gemv_splitk_layout(0), self.lib.zmi_gemv_splitk_layout(1)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -346,7 +344,7 @@ class HipEngine:
         lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows}.get(a.K, 0)
         return (lo > 0 and a.M >= lo and epi == _lib.EPI_RESIDUAL and not a.ln_w and a.pro == _lib.PRO_AUTO
                 and a.N % 64 == 0 and a.n_valid == a.N
-                and self.splitk_hdr + a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
+                and a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
 
     def _build_plan(self):
         """Invalidate the per-row-count decode plans and graphs (new weights or buffers)."""
@@ -595,16 +593,12 @@ class HipEngine:
         its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
         attn = int(self.attn_work[:4].view(torch.int32).item())
         blk, mamba, _, ffn, af, eng, leng = (int(v) for v in self.blk_err[:7].tolist())
-        sk = int(self.splitk_part[self.splitk_err:self.splitk_err + 1].view(torch.int32).item())
-        if attn or blk or mamba or ffn or af or eng or leng or sk:
+        if attn or blk or mamba or ffn or af or eng or leng:
             with torch.cuda.stream(self.stream):  # ordered with the engine's launches
                 self.attn_work[:4].zero_()
                 self.blk_err[:2].zero_()
                 self.blk_err[3:7].zero_()
-                self.splitk_part[self.splitk_err:self.splitk_err + 1].zero_()
             self.stream.synchronize()
-        if sk:
-            raise RuntimeError("gemv_splitk: an in-launch reduce workgroup timed out waiting (results are invalid)")
         if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
         if blk:
