@@ -192,9 +192,9 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     res = [it for it in gem if it[1] == _lib.EPI_RESIDUAL]
     fused_ffn = any(kd == "ffnblk" for kd, _ in plan)
     kinds = {
-        "out_proj": ([] if fused_ffn else res[0::2], d * d * 2),
+        "out_proj": ([it for it in res if it[0].K == e.H * e.hd and not fused_ffn], d * d * 2),
         "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2),
-        "fc2": (res if fused_ffn else res[1::2], d * F * 2),
+        "fc2": ([it for it in res if it[0].K == F], d * F * 2),
         "heads (LN + logits)": ([it for it in gem if it[1] == _lib.EPI_LOGITS], 9 * 1025 * d * 2),
     }
     kinds = {k: v for k, v in kinds.items() if v[0]}
@@ -223,11 +223,14 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
         blk = [it for kd, it in plan if kd == "attnblk"]
         if blk:
             us = _time_fused(e, blk, e.blk_gran, e._run_attn_block, reps)
-            nbytes = qkv_n * d * 2 + kv
-            out[f"attn_block ({form}: LN + QKV + RoPE + KV write + attention)"] = dict(
+            oproj = len(blk[0]) > 4 and blk[0][4] is not None
+            nbytes = qkv_n * d * 2 + kv + (d * d * 2 if oproj else 0)
+            what = "LN + QKV + RoPE + KV write + attention" + (" + out_proj + residual" if oproj else "")
+            note = ("QKV and out_proj weights + the layer's K/V of both rows; the launch also prefetches fc1's head"
+                    if oproj else "QKV weights + the layer's K/V of both rows; the launch also prefetches out_proj's weights")
+            out[f"attn_block ({form}: {what})"] = dict(
                 us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
-                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk),
-                note="QKV weights + the layer's K/V of both rows; the launch also prefetches out_proj's weights")
+                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk), note=note)
         # the sampler launches captured in one graph: a Python-side launch costs more than the kernel, so
         # back-to-back launches from the host would time the host
         n_s = 8 * reps

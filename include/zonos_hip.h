@@ -150,6 +150,15 @@ typedef struct ZmiPrefetch {
 } ZmiPrefetch;
 int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                       const ZmiPrefetch* prefetch, void* stream);
+/* zmi_attn_block_pf with the layer's out_proj in the same launch (8-chunk split form only: slices = 8 |
+ * ZMI_ATTNBLK_SPLIT, LayerNorm prologue): `oproj` holds the plain EPI_RESIDUAL GEMV arguments as for zmi_gemv_launch
+ * (W = out_proj weights, K = hq hd, N % 16 == 0, X = attn_out, out = the residual rows x, M = qkv->M), replacing
+ * reference _torch.py:115,140 and the residual add :100. Its workgroups follow the attention ones: they load their
+ * weight slice at their start and gather the attention output from the merging workgroups' {pair, tag} granules
+ * (in the unit's granule area) once those workgroups' flags carry the row's tag, so no out_proj launch follows.
+ * attn_out is still written. Results are bit-identical to zmi_attn_block_pf + zmi_gemv_launch(oproj). */
+int zmi_attn_block_oproj(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, unsigned* err, void* attn_out,
+                         int ldo, int slices, const ZmiPrefetch* prefetch, void* stream);
 /* zmi_attention_variant plus prefetch-only workgroups (variant 0 / 1: `prefetch->blocks` of them at the end
  * of the grid) that read prefetch->ptr[0..1][0 .. bytes) once, so the next launches (out_proj, the head of
  * fc1) find those weights in the Infinity Cache: they run on the CUs the chunks vacate, while the chunks

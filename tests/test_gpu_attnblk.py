@@ -147,3 +147,80 @@ def test_attn_block_refuses_positions_past_its_reach(slices):
                                    slices, stream_ptr()), "attn_block")
     torch.cuda.synchronize()
     assert int(err[0].item()) != 0
+
+
+@pytest.mark.parametrize("positions", [
+    (591, 592),                                 # C2 mean position, one slot
+    (0, 1),
+    (127, 128, 511, 512, 900, 1023),            # chunk / block edges and the form's last position
+    (5, -1, 300, 301, 63, 64, 700, 1000),       # 8 rows (the fused forms' default limit), an inactive row
+    (5, -1, 300, 301, 63, 64, 700, -1, 1000, 1001, 31, 32, 255, 256, 900, 17),  # 16 rows
+])
+def test_attn_block_oproj_bit_identical_to_separate_launches(positions):
+    """zmi_attn_block_oproj (the 8-chunk split form with the layer's out_proj GEMV in the same launch, its input
+    gathered from the merging workgroups' granules): q, K / V, the attention output and the new residual rows
+    bit-identical to the QKV GEMV + attention + out_proj GEMV (EPI_RESIDUAL) launches; run twice (the second launch
+    finds its own granules from the first: equal values, equal tags)."""
+    L = _lib()
+    slices = 8 | SPLIT
+    st = _setup(positions, 2056, seed=80)
+    R = st["R"]
+    ref_q, ref_k, ref_v, ref_out = _separate(st)
+    Wo = pack(rnd(D, H * HD, scale=0.03, seed=81))[0]
+    x0 = rnd(R, D, scale=2.0, seed=82)
+
+    def oargs(attn, x):
+        o = L.GemvArgs()
+        o.W, o.X, o.M, o.N, o.K, o.ldx = Wo.data_ptr(), attn.data_ptr(), R, D, H * HD, H * HD
+        o.out, o.ldo, o.n_valid = x.data_ptr(), D, D
+        return o
+
+    x_ref = x0.clone()
+    L.check(L.lib().zmi_gemv_launch(ctypes.byref(oargs(ref_out, x_ref)), L.EPI_RESIDUAL, stream_ptr()), "out_proj")
+    q = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    kc, vt = st["kc"].clone(), st["vt"].clone()
+    a = _args(st, q, kc, vt)
+    gran = torch.zeros(L.lib().zmi_attn_block_gran_words(R, HKV), dtype=torch.int64, device=DEV)
+    gran.copy_(torch.randint(0, 1 << 30, gran.shape, device=DEV) | (torch.randint(1 << 20, 1 << 30, gran.shape,
+                                                                                  device=DEV) << 32))
+    err = torch.zeros(4, dtype=torch.int32, device=DEV)
+    out = torch.zeros(R, H * HD, dtype=torch.bfloat16, device=DEV)
+    pf = L.Prefetch()
+    live = [i for i, p in enumerate(positions) if p >= 0]
+    for _ in range(2):
+        x = x0.clone()
+        L.check(L.lib().zmi_attn_block_oproj(ctypes.byref(a), ctypes.byref(oargs(out, x)), gran.data_ptr(),
+                                             err.data_ptr(), out.data_ptr(), H * HD, slices, ctypes.byref(pf),
+                                             stream_ptr()), "attn_block_oproj")
+        torch.cuda.synchronize()
+        assert int(err[0].item()) == 0, "a wait for a hand-off gave up"
+        for name, r, g in (("q", ref_q, q), ("k_cache", ref_k, kc), ("v_cache", ref_v, vt)):
+            assert torch.equal(r, g), name
+        assert torch.equal(ref_out[live], out[live]), "attention output"
+        assert torch.equal(x_ref[live], x[live]), "out_proj residual rows"
+
+
+def test_engine_fused_out_proj_keeps_codes():
+    """generate() with out_proj inside the fused block (the default) equals generate() with out_proj as its own
+    launch and with separate QKV + attention launches, across the 8-chunk form's reach (positions 900 .. 1100)."""
+    from zonos_vibes_amd.config import transformer_config
+    from zonos_vibes_amd.model import Zonos
+    cfg = transformer_config(2048, 2, 16, 4, 8192)
+    lc, n = 900, 200
+    m = Zonos.synthetic(cfg, DEV, zero_eos=True, max_seqlen=lc + n + 16, max_prefill=lc + 8)
+    g = torch.Generator().manual_seed(91)
+    cond = (torch.randn(2, lc, 2048, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    e = m.engine
+    assert any(kd == "attnblk" and it[4] is not None for kd, it in e._plan(2, "split")), "default: out_proj fused"
+    out = {}
+    for name, opts in (("fused_oproj", dict(attn_block=True, attn_oproj=True)),
+                       ("oproj_launch", dict(attn_block=True, attn_oproj=False)),
+                       ("separate", dict(attn_block=False, attn_oproj=False))):
+        for k, v in opts.items():
+            setattr(e, k, v)
+        e._build_plan()
+        out[name] = m.generate(cond, max_new_tokens=n, sampling_params=dict(temperature=0.0), progress_bar=False,
+                               chunk=64)
+        e.check_errors()
+    assert torch.equal(out["fused_oproj"], out["oproj_launch"])
+    assert torch.equal(out["fused_oproj"], out["separate"])

@@ -29,12 +29,14 @@ def main():
     ap.add_argument("--form", default="split",
                     help="split / split24 (chunk workgroups), self (self-scoring) or xs (score exchange)")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-oproj", action="store_true", help="out_proj as its own launch (engine.attn_oproj = False)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     m = Zonos.synthetic(zonos_v01_transformer(), dev, seed=0, zero_eos=True, max_seqlen=max(1040, args.pos + 24),
                         max_prefill=16)
     e = m.engine
     e.attn_block_slices = e.attn_self_slices = args.slices
+    e.attn_oproj = not args.no_oproj
     with torch.cuda.stream(e.stream):
         e.row_pos[:2] = args.pos
         e.row_kv[:2] = torch.arange(2, dtype=torch.int32, device=dev)
@@ -53,23 +55,27 @@ def main():
             for i, it in enumerate(blocks):
                 a = it[0]
                 a.reserved, a.diag = 0, (buf.data_ptr() if i == stamped else None)
+                if len(it) > 4 and it[4] is not None:  # the fused out_proj role stamps into the same buffer
+                    it[4].reserved, it[4].diag = 0, a.diag
                 e._run_attn_block(it)
                 a.diag = None
+                if len(it) > 4 and it[4] is not None:
+                    it[4].diag = None
         e.stream.synchronize()
         rows.append(buf.view(4096, 8).cpu())
     e.check_errors()
     n_qkv = 192
-    # slot 7 of an attention block: shader-clock cycles (s_memtime) between stamps 3 and 4
-    cyc = torch.cat([st[n_qkv:][st[n_qkv:, 0] > 0][:, 7] for st in rows]).double()
-    dt = torch.cat([(st[n_qkv:][st[n_qkv:, 0] > 0][:, 4] - st[n_qkv:][st[n_qkv:, 0] > 0][:, 3]) for st in rows]).double()
-    print(json.dumps(dict(phase_3_to_4_cycles=float(cyc.median()), phase_3_to_4_us=float(dt.median()) / 100.0,
-                          shader_clock_GHz=round(float((cyc / (dt * 10.0)).median()), 3))), flush=True)
     out = {}
-    for role, sl in (("qkv", slice(0, n_qkv)), ("attention", slice(n_qkv, 4096))):
+    n_att = 8 * (24 if args.form == "split24" else 8)
+    oproj = any(len(it) > 4 and it[4] is not None for it in blocks)
+    roles = [("qkv", slice(0, n_qkv)), ("attention", slice(n_qkv, n_qkv + n_att))]
+    if oproj:  # out_proj role: 0 start, 1 weights issued, 7 flags seen, 2 rows gathered, 4 chain, 5 sums, 6 epilogue
+        roles.append(("out_proj", slice(n_qkv + n_att, n_qkv + n_att + 128)))
+    for role, sl in roles:
         meds, maxs = [[] for _ in range(8)], [[] for _ in range(8)]
         if role == "attention":
             for st in rows:
-                st[:, 7] = 0
+                st[n_qkv: n_qkv + n_att, 7] = 0
         for st in rows:
             live = st[:, 0] > 0
             t0 = st[live, 0].min()
@@ -83,7 +89,7 @@ def main():
                     maxs[i].append(float(rel.max()))
         out[role] = dict(median_us=[round(sum(v) / len(v), 2) if v else None for v in meds],
                          max_us=[round(sum(v) / len(v), 2) if v else None for v in maxs])
-    print(json.dumps(dict(pos=args.pos, slices=args.slices, form=args.form, **out)), flush=True)
+    print(json.dumps(dict(pos=args.pos, slices=args.slices, form=args.form, oproj=oproj, **out)), flush=True)
 
 
 if __name__ == "__main__":

@@ -137,6 +137,8 @@ _SIGS = {
                                    c_void_p, c_int, c_void_p]),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,
                                   ctypes.POINTER(Prefetch), c_void_p]),
+    "zmi_attn_block_oproj": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p,
+                                     c_int, c_int, ctypes.POINTER(Prefetch), c_void_p]),
     "zmi_attention_work_bytes": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_partial_floats": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     "zmi_attention_chunk": (c_int, []),

@@ -773,6 +773,10 @@ struct XcG {
   static constexpr int KEYS = XCH * CH;
   static constexpr int GM = 0, GL = GM + XCH * XG, GB = GL + XCH * XG, GO = GB + XCH * XG;
   static constexpr int WORDS = GO + XCH * XG * HD;
+  // the fused out_proj role (OPROJ): the unit's output as XG HD / 2 {bf16 pair, tag} granules, then one flag per
+  // merging workgroup, after the chunk granules (only the 8-chunk form leaves room for them in the unit's area)
+  static constexpr int OG = WORDS, OF = OG + XG * HD / 2, OWORDS = OF + HD / 16;
+  static constexpr bool OPROJ_FITS = QKV_GRAN + OWORDS <= GRAN_STRIDE;
   static_assert(WORDS <= GRAN_STRIDE - QKV_GRAN, "the chunk-split granules fit the unit's area");
   static_assert(XCH >= HD / 16 && XCH % CPB == 0 && XCH <= XC_CH_MAX, "8 merging workgroups; whole 512-key blocks");
 };
@@ -788,7 +792,7 @@ struct XcImg {
   static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
 };
 
-template <int XCH>
+template <int XCH, bool OPROJ>
 __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
   using X = XcG<XCH>;
   constexpr int XC_CH = XCH, XC_GM = X::GM, XC_GL = X::GL, XC_GB = X::GB, XC_GO = X::GO;
@@ -1081,7 +1085,18 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
       }
     }
     const float rl = 1.0f / l;
-    a.out[(size_t)qi * a.ldo + (kh * XG + g) * HD + d] = (bf16_t)f2bf(acc * rl);
+    const uint32_t ov16 = f2bf(acc * rl);
+    a.out[(size_t)qi * a.ldo + (kh * XG + g) * HD + d] = (bf16_t)ov16;
+    if constexpr (OPROJ) {
+      // the same 64 values as 32 {bf16 pair, tag} granules for the out_proj role (this is wave 0: its lanes t hold
+      // (head t >> 4, dim 16 c + (t & 15))), then this workgroup's flag. The flag is only a cheap "look now" for
+      // the out_proj role's poller (64 flags instead of 2048 granules): it is not ordered after the granules,
+      // whose own tags the gather checks
+      static_assert(X::OPROJ_FITS, "the output granules fit the unit's area");
+      const uint32_t nb = (uint32_t)__shfl_xor((int)ov16, 1);
+      if ((t & 1) == 0) st_wt64(gu + QKV_GRAN + X::OG + ((g * HD + d) >> 1), (uint64_t)(ov16 | (nb << 16)) | tag64);
+      if (t == 0) st_wt64(gu + QKV_GRAN + X::OF + c, tag64);
+    }
   }
   ZMI_ASTAMP(6);
 }
@@ -1089,9 +1104,13 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
 // PRO: the projection's prologue, LayerNorm (transformer blocks) or ADDLN (the hybrid's MHA blocks:
 // layer_norm_fn(hidden, residual) with the new residual written by column block 0). SELF: the
 // attention role is xr_body (self-scoring) instead of xs_body (score exchange).
-template <int S, int PRO, int FORM>
+// OPROJ (chunk-split form, 8 chunks): a fourth role after the attention workgroups runs the layer's out_proj GEMV
+// (_torch.py:115,140 + the residual :100), its weights loaded at its start and its activation rows gathered from the
+// merging workgroups' output granules (zmi_gemv_impl.h FUSE 3), so out_proj needs no launch of its own.
+template <int S, int PRO, int FORM, bool OPROJ>
 __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
-                                                        int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf) {
+                                                        int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf,
+                                                        const ZmiGemvArgs oa, int n_op) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int n_xs = (n_units + 7) / 8 * 8 * S;
@@ -1102,16 +1121,28 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
     if constexpr (FORM == FORM_SELF)
       xr_body<S>(at, n_units, b - n_qkv, smem, gran);
     else if constexpr (FORM == FORM_SPLIT)
-      xc_body<S>(at, n_units, b - n_qkv, smem, gran);
+      xc_body<S, OPROJ>(at, n_units, b - n_qkv, smem, gran);
     else
       xs_body<S>(at, n_units, b - n_qkv, smem, gran);
+  } else if (OPROJ && b < n_qkv + n_xs + n_op) {
+    if constexpr (OPROJ) {
+      using X = XcG<S>;
+      zmi_gemv::QkvFuse fz{gran, GRAN_STRIDE};
+      fz.og_off = QKV_GRAN + X::OG;
+      fz.of_off = QKV_GRAN + X::OF;
+      fz.hkv = at.hkv;
+      fz.pos = at.pos;
+      fz.err = at.err;
+      zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_PLAIN, ZMI_EPI_RESIDUAL, 1, 3>(oa, oa.N / 8 / QG, 1,
+                                                                                       b - n_qkv - n_xs, smem, fz);
+    }
   } else
-    prefetch_body<NT>(pf, b - n_qkv - n_xs, n_pf);
+    prefetch_body<NT>(pf, b - n_qkv - n_xs - n_op, n_pf);
 }
 
-template <int S, int PRO, int FORM>
+template <int S, int PRO, int FORM, bool OPROJ = false>
 hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArgs& at, int n_units, uint64_t* gran,
-                        const ZmiPrefetch& pf, hipStream_t s) {
+                        const ZmiPrefetch& pf, hipStream_t s, const ZmiGemvArgs* oa = nullptr) {
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
   // (the wide chunk-split form with co-resident workgroups instead measured the same: profiles/r04_split24_ab.jsonl)
@@ -1121,15 +1152,16 @@ hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArg
                                spread});
   if (lds > zmi_gemv::LDS_MAX) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_block_kernel<S, PRO, FORM>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)zmi_gemv::LDS_MAX);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&attn_block_kernel<S, PRO, FORM, OPROJ>), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)zmi_gemv::LDS_MAX);
     if (attr != hipSuccess) return attr;
   }
   const int n_xs = (n_units + 7) / 8 * 8 * S;
   const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
-  hipLaunchKernelGGL((attn_block_kernel<S, PRO, FORM>), dim3((unsigned)(n_qkv + n_xs + n_pf)), dim3(NT), lds, s, a, n_cb, n_qkv, at,
-                     n_units, gran, pf, n_pf);
+  const int n_op = OPROJ ? (oa->N / 8 / QG + 7) / 8 * 8 : 0;
+  hipLaunchKernelGGL((attn_block_kernel<S, PRO, FORM, OPROJ>), dim3((unsigned)(n_qkv + n_xs + n_op + n_pf)), dim3(NT),
+                     lds, s, a, n_cb, n_qkv, at, n_units, gran, pf, n_pf, OPROJ ? *oa : a, n_op);
   return hipGetLastError();
 }
 
@@ -1139,8 +1171,9 @@ extern "C" int64_t zmi_attn_block_gran_words(int rows, int hkv) {
   return (rows <= 0 || hkv <= 0) ? -1 : (int64_t)rows * hkv * GRAN_STRIDE;
 }
 
-extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
-                                 const ZmiPrefetch* prefetch, void* stream) {
+namespace {
+int attn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, unsigned* err, void* attn_out, int ldo,
+               int slices, const ZmiPrefetch* prefetch, void* stream) {
   const ZmiGemvArgs& a = *qkv;
   if (a.K != 2048 || !a.ln_w) return zmi_fail_msg("attn_block: the QKV projection must be LayerNorm'd with K = 2048");
   const bool addln = a.pro == ZMI_PRO_ADDLN;
@@ -1187,6 +1220,18 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
   const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
   if (form == FORM_SPLIT ? (sl != 8 && sl != 24) : (sl != 4 && sl != 8))
     return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 or 24 | ZMI_ATTNBLK_SPLIT");
+  if (oproj) {  // the out_proj role (8-chunk split form, LayerNorm'd transformer blocks)
+    const ZmiGemvArgs& o = *oproj;
+    if (form != FORM_SPLIT || sl != 8 || addln)
+      return zmi_fail_msg("attn_block: the fused out_proj runs with the 8-chunk split form and a LayerNorm prologue");
+    if (o.K != a.hq * a.hd || o.N % (8 * QG) || o.n_valid != o.N || o.M != a.M || o.ln_w || o.pro != ZMI_PRO_AUTO ||
+        !o.out || o.ldo % 8 || o.ldo < o.N || o.X != attn_out)
+      return zmi_fail_msg("attn_block: out_proj must be the plain residual GEMV over the attention output "
+                          "(K = hq hd, N % 16 == 0, same rows, X = attn_out)");
+    ZMI_CHECK((launch_block<8, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s,
+                                                                   oproj)));
+    return 0;
+  }
 #define ZMI_BLK(S_, P_, F_) launch_block<S_, P_, F_>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)
 #define ZMI_BLK_P(P_)                                                                                \
   (form == FORM_SPLIT ? (sl == 8 ? ZMI_BLK(8, P_, FORM_SPLIT) : ZMI_BLK(24, P_, FORM_SPLIT))           \
@@ -1197,6 +1242,18 @@ extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* e
 #undef ZMI_BLK
   ZMI_CHECK(e);
   return 0;
+}
+}  // namespace
+
+extern "C" int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
+                                 const ZmiPrefetch* prefetch, void* stream) {
+  return attn_block(qkv, nullptr, gran, err, attn_out, ldo, slices, prefetch, stream);
+}
+
+extern "C" int zmi_attn_block_oproj(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, unsigned* err,
+                                    void* attn_out, int ldo, int slices, const ZmiPrefetch* prefetch, void* stream) {
+  if (!oproj) return zmi_fail_msg("attn_block_oproj: out_proj arguments required");
+  return attn_block(qkv, oproj, gran, err, attn_out, ldo, slices, prefetch, stream);
 }
 
 extern "C" int zmi_attn_block_max_pos(int slices) {

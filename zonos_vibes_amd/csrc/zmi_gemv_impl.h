@@ -120,6 +120,12 @@ __device__ __forceinline__ void load_gate(const float* p, float (&gz)[8]) {
 struct QkvFuse {
   uint64_t* gran;   // [M][hkv][gran_stride] u64
   int gran_stride;
+  // FUSE == 3 (zmi_attn_block's out_proj role): the GEMV's activation rows are the attention output, gathered
+  // from the units' output granules (word og_off of a unit's area: 256 {bf16 pair, tag} words, dims in order)
+  // once the unit's 8 merge-workgroup flags (word of_off + c: {0, tag}) carry the row's tag (position + 1)
+  int og_off = 0, of_off = 0, hkv = 0;
+  const int* pos = nullptr;
+  unsigned* err = nullptr;
 };
 
 // (6) fused epilogues of one group's 8 columns over a row tile, run by one wave; colsum(c, r) = the
@@ -228,8 +234,10 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   constexpr int NWV = G * W;
   constexpr int XROW = Img<K>::XROW;
   static_assert(RT == 8 || RT == 16, "row tile");
-  static_assert(!FUSE || EPI == ZMI_EPI_QKV || EPI == ZMI_EPI_STORE, "in-launch hand-off: QKV or plain store");
+  static_assert(!FUSE || EPI == ZMI_EPI_QKV || EPI == ZMI_EPI_STORE || FUSE == 3, "in-launch hand-off: QKV or plain store");
   static_assert(FUSE != 2 || NTW, "the store hand-off runs on single-tile (decode) launches");
+  static_assert(FUSE != 3 || (NTW && EPI == ZMI_EPI_RESIDUAL && PRO == PRO_PLAIN && K == 2048 && RT == 16),
+                "the gathered-input form is zmi_attn_block's out_proj role (one tile, plain, residual epilogue)");
 
   // block -> (column block, group of rpw row tiles): the groups of one column block take ids 8 apart.
   // A workgroup keeps its weight slice in registers and runs its row tiles one after the other, each
@@ -319,7 +327,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
       q_kvr = a.row_kv[row0 + (lane >> 2)];
     }
   };
-  stage_rows(true, row0, rows, X);
+  if (FUSE != 3) stage_rows(true, row0, rows, X);  // FUSE 3: the rows come from the attention's granules (below)
   stage_epi();
   __builtin_amdgcn_sched_barrier(0);
   // (2) the whole weight slice of this lane, in flight at once: one buffer descriptor per wave
@@ -334,6 +342,81 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   __builtin_amdgcn_sched_barrier(0);
   ZMI_GSTAMP(1);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // DMA pieces + epilogue operands landed
+  if constexpr (FUSE == 3) {
+    // the rows' positions (tags) in LDS first: every later check reads them without a dependent global load
+    int* qpos = reinterpret_cast<int*>(red);  // the segment-sum area, free until the MFMA chain
+    if (tid < rows) qpos[tid] = fz.pos[row0 + tid];
+    __syncthreads();
+    // (1') wave 0 polls the merge workgroups' flags of the launch's units (8 per (row, kv head); rows whose position
+    // is < 0 run no attention and contribute zero rows), sleeping between sweeps, until every unit has at least one
+    // flag up: the merges are then nearly done (64 cheap flags instead of 2048 granules while the attention runs)
+    const int n_units = rows * fz.hkv;
+    if (wave == 0) {
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+        for (int u0 = 0; u0 < n_units; u0 += 8) {  // lane = (unit u0 + lane / 8, merge workgroup lane % 8)
+          const int u = u0 + (lane >> 3), qp = u < n_units ? qpos[u / fz.hkv] : -1;
+          const bool up = qp < 0 || (uint32_t)(ld_wt64(fz.gran + (size_t)(row0 * fz.hkv + u) * fz.gran_stride + fz.of_off +
+                                                          (lane & 7)) >> 32) == (uint32_t)qp + 1u;
+          // any flag of the unit: OR over the 8 lanes of the unit (DPP within each 8-lane group)
+          float f = up ? 1.f : 0.f;
+          f = fmaxf(f, dpp_mov<DPP_XOR1>(f));
+          f = fmaxf(f, dpp_mov<DPP_XOR2>(f));
+          f = fmaxf(f, dpp_mov<DPP_HALF_MIRROR>(f));
+          ok = ok && f > 0.f;
+        }
+        if (__all(ok)) break;
+        if (spins > (1u << 18)) {
+          if (lane == 0) __hip_atomic_store(fz.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    ZMI_GSTAMP(7);
+    __syncthreads();
+    // (2') every thread polls its own {pair, tag} granules of the units' outputs (unit (r, kh), pair j: dims
+    // kh hq/hkv hd + 2 j, + 1 of row r; a unit's output is 4 heads x 128 dims = 512 columns of K: the attention block
+    // checks hq = 4 hkv, hd = 128) until each carries its row's tag, then writes them into the LDS rows. GB granules
+    // per thread per batch (2 rows x 4 kv heads: one batch), every load of a sweep issued before the first check.
+    constexpr int GB = 4;
+    for (int e0 = tid; e0 < n_units * 256; e0 += GB * NWV * 64) {
+      uint64_t gv[GB];
+      int gq[GB];
+      unsigned need = 0;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int e = e0 + NWV * 64 * i;
+        gq[i] = e < n_units * 256 ? qpos[(e >> 8) / fz.hkv] : -1;
+        gv[i] = 0ull;
+        if (gq[i] >= 0) need |= 1u << i;
+      }
+      for (unsigned spins = 0; need; ++spins) {
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+          if ((need >> i) & 1)
+            gv[i] = ld_wt64(fz.gran + (size_t)(row0 * fz.hkv + ((e0 + NWV * 64 * i) >> 8)) * fz.gran_stride + fz.og_off +
+                            ((e0 + NWV * 64 * i) & 255));
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+          if (((need >> i) & 1) && (uint32_t)(gv[i] >> 32) == (uint32_t)gq[i] + 1u) need &= ~(1u << i);
+        if (!need) break;
+        if (spins > (1u << 18)) {
+          __hip_atomic_store(fz.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int e = e0 + NWV * 64 * i;
+        if (e < n_units * 256) {
+          const int u = e >> 8, j = e & 255, r = u / fz.hkv, kh = u - r * fz.hkv;
+          *reinterpret_cast<uint32_t*>(xs + r * XROW + kh * 512 + 2 * j) = gq[i] >= 0 ? (uint32_t)gv[i] : 0u;
+        }
+      }
+    }
+  }
   for (;;) {  // the workgroup's row tiles
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);

@@ -137,6 +137,10 @@ class HipEngine:
         # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
         # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
         self.prefetch_second = "fc1"
+        # out_proj inside the chunk-split fused block (zmi_attn_block_oproj): extra workgroups load its weights
+        # during the attention chain and gather the attention output from the merging workgroups' granules, so
+        # no out_proj launch follows (identical bits; the prefetch role then warms only fc1's head)
+        self.attn_oproj = True
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
         # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
         # device: fc1's weights stream while the out_proj chain runs (identical bits). Off: it loses to the
@@ -503,10 +507,12 @@ class HipEngine:
                 xin, ln = normed((lw["ln1_w"], lw["ln1_b"])) if not fused else (self.x, (lw["ln1_w"], lw["ln1_b"]))
                 qkv = self._gemv(lw["qkv"], xin, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                  ln=ln, kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
+                oproj = fused and self._use_attn_oproj(form)
                 if fused:
                     pf = _lib.Prefetch()
                     if self.prefetch_blocks > 0:
-                        pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
+                        if not oproj:  # (the fused out_proj role loads its weights itself)
+                            pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
                         if self.prefetch_second == "qkv":
                             nw = w["heads"] if i + 1 == len(w["layers"]) else w["layers"][i + 1]["qkv"]
                         else:
@@ -514,7 +520,8 @@ class HipEngine:
                         pf.ptr[1] = nw.data_ptr()
                         pf.bytes[1] = min(nw.numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
                         pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
-                    plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form))))
+                    o_fused = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)[0] if oproj else None
+                    plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form), o_fused)))
                 else:
                     plan.append(("gemv", qkv))
                     apf = None
@@ -529,7 +536,11 @@ class HipEngine:
                     plan.append(("ffneng", self._ffn_engine_args(lw, i, rows)))
                     continue
                 o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
-                if self._use_ffn_block(rows):
+                if oproj:  # out_proj ran inside the fused block
+                    xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
+                    plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
+                                                    self.F, ln=ln)))
+                elif self._use_ffn_block(rows):
                     o_item[0].row_pos = self.row_pos.data_ptr()
                     f_item = self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
                                         ln=(lw["ln2_w"], lw["ln2_b"]))
@@ -569,10 +580,20 @@ class HipEngine:
             None if pf is None else ctypes.byref(pf), self.sptr), "attention")
 
     def _run_attn_block(self, item):
-        a, i, pf, slices = item
+        a, i, pf, slices = item[:4]
+        o = item[4] if len(item) > 4 else None
+        if o is not None:
+            _lib.check(self.lib.zmi_attn_block_oproj(ctypes.byref(a), ctypes.byref(o), self.blk_gran[i].data_ptr(),
+                                                     self.blk_err.data_ptr(), self.attn.data_ptr(), self.H * self.hd,
+                                                     slices, ctypes.byref(pf), self.sptr), "attn_block_oproj")
+            return
         _lib.check(self.lib.zmi_attn_block_pf(ctypes.byref(a), self.blk_gran[i].data_ptr(), self.blk_err.data_ptr(),
                                               self.attn.data_ptr(), self.H * self.hd, slices,
                                               ctypes.byref(pf), self.sptr), "attn_block")
+
+    def _use_attn_oproj(self, form: str) -> bool:
+        """out_proj inside the fused block: the 8-chunk split form of a LayerNorm'd transformer block."""
+        return self.attn_oproj and form == "split" and not self.hybrid and self.H * self.hd == self.d
 
     def _run_attn_ffn(self, item):
         a, o, f, i = item
