@@ -469,7 +469,10 @@ def time_long_utterance(dev, n_new: int = 86 * 30, engine_opts: dict | None = No
     cfg = zonos_v01_transformer()
     m = Zonos.synthetic(cfg, dev, seed=0, zero_eos=True, max_seqlen=LC + n_new + 9, max_prefill=LC + 1)
     for k, v in (engine_opts or {}).items():  # A/B knobs (tools/bench_long.py)
-        setattr(m.engine, k, tuple(v) if isinstance(v, list) else v)
+        if k.startswith("opt_"):  # library launch knobs: opt_attnblk_spread -> zmi_set_option(OPT_ATTNBLK_SPREAD)
+            _lib.check(m.engine.lib.zmi_set_option(getattr(_lib, "OPT_" + k[4:].upper()), int(v)), k)
+        else:
+            setattr(m.engine, k, tuple(v) if isinstance(v, list) else v)
     m.engine._build_plan()
     cond = cond_tensor(1, cfg.backbone.d_model, dev)
 

@@ -374,10 +374,13 @@ int zmi_version(void);
  *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
  *   ZMI_OPT_DAC_WIDE (default 1): DAC convs on 256-row time tiles (512-thread workgroups) when the output has at
  *          least ZMI_OPT_DAC_WIDE_MIN (default 256) 256-row x 32-channel units; 0 = always 128-row tiles, 2 = always
- *          256. */
+ *          256.
+ *   ZMI_OPT_ATTNBLK_SPREAD (default 5): zmi_attn_block's workgroups reserve LDS so the launch spreads over the chip;
+ *          bits 0-1 for the 8-chunk split / score-exchange / self forms, bits 2-3 for the 24-chunk split form:
+ *          0 = no reserve, 1 = one workgroup per CU, 2 = at most two. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
-       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_COUNT = 12 };
+       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_COUNT = 13 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

@@ -1022,52 +1022,70 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
     }
     ZMI_ASTAMP(5);
   }
-  // (8) dims 16 c .. + 15 of the unit's output: every chunk's partial, l and M_j (gathered), the block
-  // recursion of zmi_attn_merge.h, one thread per (head, dim)
-  if (c < HD / 16 && t < XG * 16) {
-    const int g = t >> 4, d = 16 * c + (t & 15);
-    uint64_t ov[XC_CH], lv[XC_CH], mv[XC_CH / CPB];
-    static_assert(2 * XC_CH + XC_CH / CPB <= 64, "one pending bit per granule");
-    uint64_t pend = 0;
+  // (8) dims 16 c .. + 15 of the unit's output: every chunk's partial, l and M_j, gathered by all eight waves (wave w
+  // polls chunks w, w + 8, w + 16 and block maximum w, lane = (head, dim) as below) into LDS (the score / partial areas,
+  // free after (7)), then the block recursion of zmi_attn_merge.h by wave 0, one lane per (head, dim). Spreading the
+  // polls over the waves keeps each wave's granules in flight to a few (the 24-chunk form held all 54 per lane).
+  if (c < HD / 16) {
+    constexpr int KPW = (XC_CH + DNW - 1) / DNW, NBLK = XC_CH / CPB;
+    static_assert(NBLK <= DNW && 2 * KPW + 1 <= 32, "one block maximum per wave; one pending bit per granule");
+    float* mO = reinterpret_cast<float*>(smem + XcImg::OP);   // [XC_CH][XG x 16] partials of the (head, dim)s
+    float* mL = reinterpret_cast<float*>(smem + XcImg::SC);   // [XC_CH][XG] chunk l
+    float* mM = mL + XC_CH * XG;                              // [NBLK][XG] block M_j
+    static_assert((size_t)XC_CH * XG * 16 * 4 <= XcImg::MJ - XcImg::OP &&
+                  (size_t)(XC_CH + NBLK) * XG * 4 <= XcImg::PB - XcImg::SC, "the merge staging fits the freed areas");
+    __syncthreads();  // (7)'s partial reads are done before its LDS is reused
+    const int l64 = t & 63, g = l64 >> 4, d = 16 * c + (l64 & 15);
+    uint64_t ov[KPW], lv[KPW], mv = 0ull;
+    unsigned pend = 0;
 #pragma unroll
-    for (int k = 0; k < XC_CH; ++k)
-      if (k < nc) pend |= 3ull << (2 * k);
-#pragma unroll
-    for (int j = 0; j < XC_CH / CPB; ++j)
-      if (j * CPB < nc) pend |= 1ull << (2 * XC_CH + j);
+    for (int i = 0; i < KPW; ++i)
+      if (wave + DNW * i < nc) pend |= 3u << (2 * i);
+    if (wave < NBLK && wave * CPB < nc) pend |= 1u << (2 * KPW);
     for (unsigned spins = 0; pend; ++spins) {
 #pragma unroll
-      for (int k = 0; k < XC_CH; ++k) {
-        if ((pend >> (2 * k)) & 1) ov[k] = ld_wt64(gx + XC_GO + (k * XG + g) * HD + d);
-        if ((pend >> (2 * k + 1)) & 1) lv[k] = ld_wt64(gx + XC_GL + k * XG + g);
+      for (int i = 0; i < KPW; ++i) {
+        const int k = wave + DNW * i;
+        if ((pend >> (2 * i)) & 1) ov[i] = ld_wt64(gx + XC_GO + (k * XG + g) * HD + d);
+        if ((pend >> (2 * i + 1)) & 1) lv[i] = ld_wt64(gx + XC_GL + k * XG + g);
       }
+      if ((pend >> (2 * KPW)) & 1) mv = ld_wt64(gx + XC_GB + wave * CPB * XG + g);
 #pragma unroll
-      for (int j = 0; j < XC_CH / CPB; ++j)
-        if ((pend >> (2 * XC_CH + j)) & 1) mv[j] = ld_wt64(gx + XC_GB + j * CPB * XG + g);
-#pragma unroll
-      for (int k = 0; k < XC_CH; ++k) {
-        if (((pend >> (2 * k)) & 1) && tag_of(ov[k]) == tag) pend &= ~(1ull << (2 * k));
-        if (((pend >> (2 * k + 1)) & 1) && tag_of(lv[k]) == tag) pend &= ~(1ull << (2 * k + 1));
+      for (int i = 0; i < KPW; ++i) {
+        if (((pend >> (2 * i)) & 1) && tag_of(ov[i]) == tag) pend &= ~(1u << (2 * i));
+        if (((pend >> (2 * i + 1)) & 1) && tag_of(lv[i]) == tag) pend &= ~(1u << (2 * i + 1));
       }
-#pragma unroll
-      for (int j = 0; j < XC_CH / CPB; ++j)
-        if (((pend >> (2 * XC_CH + j)) & 1) && tag_of(mv[j]) == tag) pend &= ~(1ull << (2 * XC_CH + j));
-      if (!pend) break;
+      if (((pend >> (2 * KPW)) & 1) && tag_of(mv) == tag) pend &= ~(1u << (2 * KPW));
+      if (__all(pend == 0)) break;
       if (spins > XS_SPIN) {
         give_up(a);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
 #pragma unroll
-    for (int k = 0; k < XC_CH; ++k) {
-      if (k >= nc) continue;  // (not break: the unrolled arrays stay in registers)
-      const float o = __uint_as_float((uint32_t)ov[k]), lk = __uint_as_float((uint32_t)lv[k]);
+    for (int i = 0; i < KPW; ++i) {
+      const int k = wave + DNW * i;
+      if (k < nc) {
+        mO[k * (XG * 16) + l64] = __uint_as_float((uint32_t)ov[i]);
+        if ((l64 & 15) == 0) mL[k * XG + g] = __uint_as_float((uint32_t)lv[i]);
+      }
+    }
+    if (wave < NBLK && wave * CPB < nc && (l64 & 15) == 0) mM[wave * XG + g] = __uint_as_float((uint32_t)mv);
+    __syncthreads();
+  }
+  if (c < HD / 16 && t < XG * 16) {
+    const int g = t >> 4, d = 16 * c + (t & 15);
+    const float* mO = reinterpret_cast<const float*>(smem + XcImg::OP);
+    const float* mL = reinterpret_cast<const float*>(smem + XcImg::SC);
+    const float* mM = mL + XC_CH * XG;
+    float acc = 0.f, l = 0.f, ob = 0.f, lb = 0.f, mprev = 0.f, mb = 0.f;
+    for (int k = 0; k < nc; ++k) {
+      const float o = mO[k * (XG * 16) + t], lk = mL[k * XG + g];
       if (k % CPB == 0) {
         ob = o;
         lb = lk;
-        mb = __uint_as_float((uint32_t)mv[k / CPB]);
+        mb = mM[(k / CPB) * XG + g];
       } else {
         ob += o;
         lb += lk;
@@ -1146,7 +1164,11 @@ hipError_t launch_block(const ZmiGemvArgs& a, int n_cb, int n_qkv, const AttnArg
   // at least half the CU's LDS: one workgroup per CU, so the ~256 workgroups spread over the chip
   // instead of sharing a CU's ~64 KB of loads in flight
   // (the wide chunk-split form with co-resident workgroups instead measured the same: profiles/r04_split24_ab.jsonl)
-  const size_t spread = zmi_gemv::LDS_MAX / 2 + 1024;
+  // (ZMI_OPT_ATTNBLK_SPREAD bits 0-1: the floor of the 8-chunk / score-exchange / self forms, bits 2-3: of the
+  // 24-chunk form, whose 384 workgroups otherwise leave 128 of its attention workgroups waiting for projection CUs;
+  // 0 = none, 1 = one workgroup per CU, 2 = at most two)
+  const int fl = (zmi_option(ZMI_OPT_ATTNBLK_SPREAD) >> (S == 24 ? 2 : 0)) & 3;
+  const size_t spread = fl == 1 ? zmi_gemv::LDS_MAX / 2 + 1024 : (fl == 2 ? zmi_gemv::LDS_MAX / 3 + 1024 : 0);
   const size_t lds = std::max({zmi_gemv::Img<2048>::bytes(a.M, DNW, QRT, PRO),
                                FORM == FORM_SELF ? XrImg<S>::BYTES : (FORM == FORM_SPLIT ? XcImg::BYTES : XsImg<S>::BYTES),
                                spread});
