@@ -229,7 +229,9 @@ int zmi_delay_revert(const ZmiSlots* slots, int slot, int64_t* out, int t_out, v
 
 /* ---------------------------------------------------------------------------------------
  * DAC 44.1 kHz decoder (DACAutoencoder.decode, autoencoder.py:25-27 -> transformers DacModel).
- * Activations are fp16, channels-last [T][C]; weights fp16 packed per tap [tap][Co][Ci].
+ * Activations are fp16, channels-last [T][C]; weights fp16 channel-blocked per tap [tap][Ci/32][Co][32] (one
+ * 32-channel step of 16 output channels is 1 KiB contiguous: one LDS-DMA piece), except 1x1 convs (taps == 1):
+ * [Co][Ci].
  * ------------------------------------------------------------------------------------- */
 /* z[t][c] = sum_i (out_proj_i(codebook_i[codes[i][t]]))   (modeling_dac.py:347-371)          */
 int zmi_dac_from_codes(const int64_t* codes, int T, const float* codebooks, const float* proj_w,
@@ -251,12 +253,12 @@ int zmi_dac_vq(const float* latents, int t, const float* in_w, const float* in_b
                const float* codebooks_n, const float* codebooks_n2, const float* out_w, const float* out_b,
                int64_t* codes, void* stream);
 /* polyphase ConvTranspose1d(c_in, c_out, k = 2 stride, stride, pad) of a DacDecoderBlock (modeling_dac.py:222-240),
- * every phase in one launch: w_phases fp16 [stride][2][c_out][c_in], phase rho's taps (rho + pad) % stride and
+ * every phase in one launch: w_phases fp16 [stride][2][c_in/32][c_out][32], phase rho's taps (rho + pad) % stride and
  * + stride, transposed; out [stride t_in][c_out] raw and / or Snake'd with alpha. */
 int zmi_dac_conv_t(const void* x, int t_in, int c_in, const void* w_phases, const float* bias, int c_out, int stride,
                    int pad, void* out_raw, void* out_snake, const float* alpha, void* stream);
 /* final Snake'd [T][c_in] -> conv k7 (c_in->1) -> tanh -> f32 [T]  (modeling_dac.py:438-441), on the
- * MFMA conv kernel: w_pad fp16 [7][32][c_in] (output channel 0 = the filter, 1..31 zero), bias_pad f32 [32]. */
+ * MFMA conv kernel: w_pad fp16 [7][c_in/32][32][32] (output channel 0 = the filter, 1..31 zero), bias_pad f32 [32]. */
 int zmi_dac_conv_out(const void* x, int t, int c_in, const void* w_pad, const float* bias_pad, float* out,
                      void* stream);
 
@@ -377,10 +379,15 @@ int zmi_version(void);
  *          256.
  *   ZMI_OPT_ATTNBLK_SPREAD (default 5): zmi_attn_block's workgroups reserve LDS so the launch spreads over the chip;
  *          bits 0-1 for the 8-chunk split / score-exchange / self forms, bits 2-3 for the 24-chunk split form:
- *          0 = no reserve, 1 = one workgroup per CU, 2 = at most two. */
+ *          0 = no reserve, 1 = one workgroup per CU, 2 = at most two.
+ *   ZMI_OPT_DAC_STAGE (default 13): DAC convs on the staged K loop (one barrier per 32-channel step x all taps, one
+ *          512-thread workgroup per CU); bit 0 the k7 convs, bit 1 the 1x1 convs, bit 2 the transposed convs,
+ *          bit 3 512-row time tiles for the k7 convs (256 otherwise).
+ *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
-       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_COUNT = 13 };
+       ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
+       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_COUNT = 15 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

@@ -269,9 +269,12 @@ def test_dac_decode_c5_length_windows_bit_identical():
 
 @pytest.mark.parametrize("frames", [97, 861])
 def test_dac_wide_time_tiles_bit_identical(frames):
-    """The DAC convs on 256-row time tiles (512-thread workgroups, ZMI_OPT_DAC_WIDE = 2), on 128-row tiles (0) and
-    the default per-conv choice (1) give the same bits, decode and the encoder's latents: a conv output's K order and MFMA
-    chain do not depend on the tile."""
+    """The DAC convs on 256-row time tiles (512-thread workgroups, ZMI_OPT_DAC_WIDE = 2), on 128-row tiles (0), the
+    per-conv choice (1), and on the staged K loop (conv_stage_kernel: ZMI_OPT_DAC_STAGE bits for the k7 / 1x1 /
+    transposed convs and 512-row k7 tiles, forced onto every eligible conv with ZMI_OPT_DAC_STAGE_MIN = 1, and the
+    default) give the
+    same bits, decode and the encoder's latents: a conv output's K order and MFMA chain do not depend on the tile
+    or on how many K steps share a barrier."""
     from zonos_vibes_amd import _lib
     from zonos_vibes_amd.autoencoder import DACAutoencoder
     from tests.helpers import synthetic_wav
@@ -279,16 +282,21 @@ def test_dac_wide_time_tiles_bit_identical(frames):
     codes = torch.randint(0, 1024, (1, 9, frames), generator=torch.Generator().manual_seed(frames)).to(DEV)
     wav_in = synthetic_wav(1, frames * 512, seed=3).to(DEV)
     lib = _lib.lib()
-    old = lib.zmi_get_option(_lib.OPT_DAC_WIDE)
+    knobs = (_lib.OPT_DAC_WIDE, _lib.OPT_DAC_STAGE, _lib.OPT_DAC_STAGE_MIN)
+    old = [lib.zmi_get_option(k) for k in knobs]
+    cases = [(0, 0, 256), (2, 0, 256), (1, 0, 256), (1, 7, 1), (1, 15, 1), (1, 9, 256), tuple(old)]
     outs = {}
     try:
-        for wide in (0, 2, 1):
-            _lib.check(lib.zmi_set_option(_lib.OPT_DAC_WIDE, wide))
+        for case in cases:
+            for k, v in zip(knobs, case):
+                _lib.check(lib.zmi_set_option(k, v))
             lat = torch.empty(frames, 1024, dtype=torch.float32, device=DEV)
             ae.encode_latents(wav_in[0, 0].contiguous(), lat)
-            outs[wide] = (ae.decode(codes).cpu(), lat.cpu())
+            outs[case] = (ae.decode(codes).cpu(), lat.cpu())
     finally:
-        lib.zmi_set_option(_lib.OPT_DAC_WIDE, old)
-    for wide in (2, 1):
-        assert torch.equal(outs[wide][0], outs[0][0]), wide
-        assert torch.equal(outs[wide][1], outs[0][1]), wide
+        for k, v in zip(knobs, old):
+            lib.zmi_set_option(k, v)
+    base = outs[cases[0]]
+    for case in cases[1:]:
+        assert torch.equal(outs[case][0], base[0]), case
+        assert torch.equal(outs[case][1], base[1]), case

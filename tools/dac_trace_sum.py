@@ -8,9 +8,10 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Time
 agg = collections.OrderedDict()
 for r in rows:
     n = r['Kernel_Name']
-    if 'conv_kernel' not in n:
+    if 'conv_kernel' not in n and 'conv_stage_kernel' not in n:
         continue
-    key = (n[n.index('conv_kernel'):n.index('conv_kernel') + 17], r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])
+    i = n.index('conv_')
+    key = (n[i:n.index('>', i) + 1], r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])
     agg.setdefault(key, []).append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
 tot = sum(sum(v) for v in agg.values())
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):

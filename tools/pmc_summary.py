@@ -72,8 +72,26 @@ def mfma(path):
     print(json.dumps({"kernels": out}, indent=1))
 
 
+def per_kernel(path):
+    """Every counter of the pass, averaged per dispatch, per kernel (kernels ordered by total duration)."""
+    per = defaultdict(lambda: defaultdict(float))
+    dur = defaultdict(dict)
+    for row in csv.DictReader(open(path)):
+        k = _short(row["Kernel_Name"])
+        per[k][row["Counter_Name"]] += float(row["Counter_Value"])
+        dur[k][row["Dispatch_Id"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3
+    out = {}
+    for k, c in sorted(per.items(), key=lambda kv: -sum(dur[kv[0]].values())):
+        n = len(dur[k])
+        out[k] = {"dispatches": n, "avg_us": round(sum(dur[k].values()) / n, 2),
+                  **{name: round(v / n, 1) for name, v in sorted(c.items())}}
+    print(json.dumps({"kernels": out}, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "--mfma":
         mfma(sys.argv[2])
+    elif sys.argv[1] == "--per-kernel":
+        per_kernel(sys.argv[2])
     else:
         main(sys.argv[1], sys.argv[2], int(sys.argv[3]))

@@ -30,6 +30,8 @@ OPT_ENG_DELAY = 9
 OPT_DAC_WIDE = 10
 OPT_DAC_WIDE_MIN = 11
 OPT_ATTNBLK_SPREAD = 12
+OPT_DAC_STAGE = 13
+OPT_DAC_STAGE_MIN = 14
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3

@@ -41,6 +41,15 @@ def _fold_weight_norm(sd: dict) -> dict:
     return out
 
 
+def _blocked(w: torch.Tensor) -> torch.Tensor:
+    """[..., co, ci] conv weights -> fp16 channel-blocked [..., ci / 32, co, 32]: the layout zmi_dac_conv* read for
+    convs with more than one tap, in which one 32-channel step of 16 output channels (one LDS-DMA piece, 16 x 64 B)
+    is 1 KiB contiguous (1x1 convs keep [co][ci], include/zonos_hip.h)."""
+    co, ci = w.shape[-2], w.shape[-1]
+    assert ci % 32 == 0, ci
+    return w.reshape(*w.shape[:-1], ci // 32, 32).transpose(-3, -2).contiguous().half()
+
+
 class DACAutoencoder:
     codebook_size = 1024
     num_codebooks = N_CODEBOOKS
@@ -66,8 +75,9 @@ class DACAutoencoder:
     def _prepare(self, sd: dict):
         f32 = lambda t: t.to(self.dev, torch.float32).contiguous()  # noqa: E731
 
-        def conv_w(w):  # [co][ci][k] -> [k][co][ci] fp16
-            return w.to(self.dev, torch.float32).permute(2, 0, 1).contiguous().half()
+        def conv_w(w):  # [co][ci][k] -> channel-blocked [k][ci / 32][co][32] fp16 (_blocked); 1x1: [1][co][ci]
+            w = w.to(self.dev, torch.float32).permute(2, 0, 1)
+            return w.contiguous().half() if w.shape[0] == 1 else _blocked(w)
 
         with torch.cuda.stream(self.stream):
             q = "quantizer.quantizers."
@@ -76,6 +86,7 @@ class DACAutoencoder:
                                        for i in range(N_CODEBOOKS)]).contiguous()
             self.proj_b = torch.stack([f32(sd[f"{q}{i}.out_proj.bias"]) for i in range(N_CODEBOOKS)]).contiguous()
             self.c1_w, self.c1_b = conv_w(sd["decoder.conv1.weight"]), f32(sd["decoder.conv1.bias"])
+            self.c1_cin, self.c1_cout = sd["decoder.conv1.weight"].shape[1], sd["decoder.conv1.weight"].shape[0]
             self.blocks = []
             for j, s in enumerate(STRIDES):
                 p = f"decoder.block.{j}."
@@ -87,7 +98,7 @@ class DACAutoencoder:
                     phases.append(torch.stack([wt[:, :, k0].t(), wt[:, :, k0 + s].t()]))  # [2][cout][cin]
                 blk = dict(stride=s, pad=pad, cin=wt.shape[0], cout=wt.shape[1],
                            alpha=f32(sd[p + "snake1.alpha"]).reshape(-1),
-                           wt=torch.stack(phases).half().contiguous(), bt=f32(sd[p + "conv_t1.bias"]), res=[])
+                           wt=_blocked(torch.stack(phases)), bt=f32(sd[p + "conv_t1.bias"]), res=[])
                 for u in range(3):
                     r = p + f"res_unit{u + 1}."
                     blk["res"].append(dict(a1=f32(sd[r + "snake1.alpha"]).reshape(-1),
@@ -99,7 +110,7 @@ class DACAutoencoder:
             w2 = f32(sd["decoder.conv2.weight"])                              # [1][96][7]
             self.out_w = torch.zeros(7, 32, w2.shape[1], device=self.dev)     # [k][co padded to 32][ci]
             self.out_w[:, 0, :] = w2[0].t()
-            self.out_w = self.out_w.half().contiguous()
+            self.out_w = _blocked(self.out_w)
             self.out_b = torch.zeros(32, device=self.dev)
             self.out_b[0] = f32(sd["decoder.conv2.bias"]).reshape(-1)[0]
             self.has_encoder = "encoder.conv1.weight" in sd
@@ -111,7 +122,7 @@ class DACAutoencoder:
         w1 = f32(sd["encoder.conv1.weight"])                                  # [64][1][7]
         col = torch.zeros(1, w1.shape[0], 32, device=self.dev)
         col[0, :, :7] = w1[:, 0, :]
-        self.e1_w, self.e1_b = col.half().contiguous(), f32(sd["encoder.conv1.bias"])
+        self.e1_w, self.e1_b = col.half().contiguous(), f32(sd["encoder.conv1.bias"])  # 1x1: [1][co][ci]
         self.eblocks = []
         c = w1.shape[0]
         for j, s in enumerate(ENC_STRIDES):
@@ -133,10 +144,11 @@ class DACAutoencoder:
                     if 0 <= k < 2 * s:
                         wp[a, :, jj, :] = wt[:, :, k]
             self.eblocks.append(dict(stride=s, c=c, res=res, alpha=f32(sd[p + "snake1.alpha"]).reshape(-1),
-                                     w=wp.reshape(3, 2 * c, s * c).half().contiguous(), b=f32(sd[p + "conv1.bias"])))
+                                     w=_blocked(wp.reshape(3, 2 * c, s * c)), b=f32(sd[p + "conv1.bias"])))
             c *= 2
         self.e_final_alpha = f32(sd["encoder.snake1.alpha"]).reshape(-1)
         self.e2_w, self.e2_b = conv_w(sd["encoder.conv2.weight"]), f32(sd["encoder.conv2.bias"])
+        self.e2_cin, self.e2_cout = sd["encoder.conv2.weight"].shape[1], sd["encoder.conv2.weight"].shape[0]
         q = "quantizer.quantizers."
         self.vq_in_w = torch.stack([f32(sd[f"{q}{i}.in_proj.weight"]).reshape(8, -1) for i in range(N_CODEBOOKS)])
         self.vq_in_b = torch.stack([f32(sd[f"{q}{i}.in_proj.bias"]) for i in range(N_CODEBOOKS)]).contiguous()
@@ -165,9 +177,9 @@ class DACAutoencoder:
         z = S2
         _lib.check(self.lib.zmi_dac_from_codes(codes.data_ptr(), T, self.codebooks.data_ptr(), self.proj_w.data_ptr(),
                                                self.proj_b.data_ptr(), z.data_ptr(), self.sptr), "from_codes")
-        c = self.c1_w.shape[1]
+        c = self.c1_cout
         # conv1 (k7, pad 3) -> Snake of block 0 (its only consumer is block 0's ConvTranspose)
-        self._conv(z, T, self.c1_w.shape[2], self.c1_w, self.c1_b, c, 7, 1, -3, T, 1, 0, T, snake=SA,
+        self._conv(z, T, self.c1_cin, self.c1_w, self.c1_b, c, 7, 1, -3, T, 1, 0, T, snake=SA,
                    alpha=self.blocks[0]["alpha"])
         t = T
         xin, xalt = SA, SB
@@ -253,7 +265,7 @@ class DACAutoencoder:
                        raw=H if j + 1 < len(self.eblocks) else None, snake=S2, alpha=nxt)
             SA, S2 = S2, SA
             t = tn
-        self._conv(SA, t, self.e2_w.shape[2], self.e2_w, self.e2_b, self.e2_w.shape[1], 3, 1, -1, t, 1, 0, t, f32=lat)
+        self._conv(SA, t, self.e2_cin, self.e2_w, self.e2_b, self.e2_cout, 3, 1, -1, t, 1, 0, t, f32=lat)
 
     @torch.inference_mode()
     def encode(self, wav: torch.Tensor) -> torch.Tensor:
