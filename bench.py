@@ -526,7 +526,13 @@ def time_hybrid(dev, n_new: int) -> dict:
     el = time.perf_counter() - t0
     assert codes.shape[-1] == n_new
     e = m.engine
-    s_len = e.prefill(0, cond, None, n_new, SamplingParams(temperature=0.0))
+    e.prefill(0, cond, None, n_new, SamplingParams(temperature=0.0))
+    e.release(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s_len = e.prefill(0, cond, None, n_new, SamplingParams(temperature=0.0))  # the Lc + 1 = 161-row prefill
+    torch.cuda.synchronize()
+    prefill_ms = (time.perf_counter() - t0) * 1e3
     lead, steps = max(0, n_new // 2 - 32), 64
     e.step(lead, slots=1)
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -542,6 +548,7 @@ def time_hybrid(dev, n_new: int) -> dict:
     out = {"config": f"C4: Zonos-v0.1-hybrid dims (46 layers: 41 Mamba2 + MHA at 9/18/27/36/45), batch 1, Lc={LC}, "
                      f"{n_new} frames, greedy, EOS suppressed, + DAC decode",
            "rtf": round(n_new * DAC_HOP / DAC_SAMPLE_RATE / el, 3), "utterance_ms": round(el * 1e3, 1),
+           "prefill_ms": round(prefill_ms, 2), "prefill_rows": 2 * s_len,
            "decode_step_us": round(us, 1), "decode_step_pos": pos, "step_bytes": b,
            "decode_step_hbm_frac": round(b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
            "parity": "unpinned (mamba-ssm absent); held to oracle/hybrid_cpu.py by tests/test_gpu_hybrid.py"}

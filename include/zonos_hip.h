@@ -320,6 +320,11 @@ int zmi_mamba2_step(const ZmiMamba2Args* args, void* stream);
 /* Prefill from an empty state: M / seq_len sequences of seq_len rows (causal_conv1d_fn +
  * mamba_chunk_scan_combined of Mamba2.forward), leaving each sequence's final state and conv ring. */
 int zmi_mamba2_scan(const ZmiMamba2Args* args, int seq_len, void* stream);
+/* The same prefill, parallel form (the one HybridEngine runs): a conv + SiLU / dt launch into `ws`, then the
+ * recurrence on 4 workgroups per (sequence, head), fused multiply-adds (fp32 rounding differs from
+ * zmi_mamba2_scan's; both are checked against the oracle). ws: >= zmi_mamba2_scan_ws_bytes(M, d_ssm, nheads). */
+int zmi_mamba2_scan_ws(const ZmiMamba2Args* args, int seq_len, void* ws, int64_t ws_bytes, void* stream);
+int64_t zmi_mamba2_scan_ws_bytes(int m, int d_ssm, int nheads);
 /* layer_norm_fn(hidden, w, b, residual, prenorm=True): s = hidden + residual (fp32; hidden may be NULL:
  * s = residual), residual <- bf16(s) if store_residual, out = LayerNorm(s) bf16; k in {512 .. 4096}. */
 int zmi_add_layernorm(const void* hidden, int ldh, void* residual, int ldr, int m, int k, const void* w,
@@ -383,11 +388,13 @@ int zmi_version(void);
  *   ZMI_OPT_DAC_STAGE (default 13): DAC convs on the staged K loop (one barrier per 32-channel step x all taps, one
  *          512-thread workgroup per CU); bit 0 the k7 convs, bit 1 the 1x1 convs, bit 2 the transposed convs,
  *          bit 3 512-row time tiles for the k7 convs (256 otherwise).
- *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups. */
+ *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups.
+ *   ZMI_OPT_SCAN_PQ (default 4): zmi_mamba2_scan_ws workgroups per (sequence, head) (1, 2 or 4; each thread then
+ *          owns 4 / PQ head dims x 8 state columns). */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
        ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
-       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_COUNT = 15 };
+       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_COUNT = 16 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

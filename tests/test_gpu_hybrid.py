@@ -122,9 +122,12 @@ def test_mamba2_step_matches_oracle():
             assert torch.equal(dev["ring"][r, (p - k) & 3].cpu(), ring[r, (p - k) & 3])
 
 
-@pytest.mark.parametrize("seq_len", [1, 3, 45])
-def test_mamba2_scan_matches_oracle(seq_len):
-    """Mamba2.forward from an empty cache for two sequences (tile edges at 32 positions)."""
+@pytest.mark.parametrize("form", ["scan", "scan_ws"])
+@pytest.mark.parametrize("seq_len", [1, 3, 45, 161])
+def test_mamba2_scan_matches_oracle(seq_len, form):
+    """Mamba2.forward from an empty cache for two sequences (tile edges at 32 positions; 161 = C4's prefill), by the
+    single-workgroup scan (zmi_mamba2_scan) and the parallel form the engine runs (zmi_mamba2_scan_ws: conv launch
+    + 4 workgroups per (sequence, head), fused multiply-adds): y within 4 bf16 ulps, the final state within 1."""
     L, lib = _lib()
     md = tiny_hybrid().backbone.mamba2_dims()
     cw, cb, dtb, A, D = _mamba_params(md, 21)
@@ -137,7 +140,13 @@ def test_mamba2_scan_matches_oracle(seq_len):
     rp = torch.arange(seq_len, dtype=torch.int32, device=DEV).repeat(2)
     rk = torch.tensor([0] * seq_len + [1] * seq_len, dtype=torch.int32, device=DEV)
     a = _args(L, md, zxd, dev["cw"], dev["cb"], dev["dtb"], dev["A"], dev["D"], ring, ssm, y, 2 * seq_len, rp, rk)
-    L.check(lib.zmi_mamba2_scan(ctypes.byref(a), seq_len, 0), "scan")
+    if form == "scan":
+        L.check(lib.zmi_mamba2_scan(ctypes.byref(a), seq_len, 0), "scan")
+    else:
+        nb = int(lib.zmi_mamba2_scan_ws_bytes(2 * seq_len, md["d_ssm"], md["nheads"]))
+        ws = torch.full((nb,), 0xA5, dtype=torch.uint8, device=DEV)  # stale workspace must not matter
+        L.check(lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb, 0), "scan_ws")
+        assert lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb - 1, 0) != 0  # too small: refused
     torch.cuda.synchronize()
     ry, rs, rconv = mamba2_scan_ref(zx, cw, cb, dtb, A, D, md)
     assert _ulps(y.view(2, seq_len, -1), ry) <= 4.0

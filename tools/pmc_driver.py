@@ -8,6 +8,7 @@ C2 mean position, on the synthetic Zonos-v0.1 engine (B = 1, two CFG rows).
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention)
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py ffnblk      (fused out_proj + fc1)
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py engine      (zmi_layer_engine, layers 0..24)
+    rocprofv3 --pmc SQ_LDS_BANK_CONFLICT ... -- python tools/pmc_driver.py step   (the whole default decode step)
 then tools/pmc_summary.py turns the counter CSV into the per-launch JSON kept under profiles/.
 """
 import ctypes
@@ -43,7 +44,7 @@ def main(which: str, reps: int = 2):
     if which == "ffnblk":  # the fused out_proj + fc1 launch (off by default)
         e.ffn_block = True
         e._build_plan()
-    if which != "engine":
+    if which not in ("engine", "step"):
         e.layer_engine = False  # the launch plan's kernels
         e._build_plan()
     plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
@@ -65,6 +66,8 @@ def main(which: str, reps: int = 2):
             for kind, it in plan:
                 if kind == "attnblk":
                     e._run_attn_block(it)
+        elif which == "step":  # the whole C2 decode step (launch plan + sampler) at POS, position held
+            e.enqueue_step(form=e._segments(1, 1)[0][1])
         elif which == "engine":  # the layer engine launches with the next layer's QKV (granules fresh per rep)
             e.lay_gran.zero_()
             for kind, it in plan:

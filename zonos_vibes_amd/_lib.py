@@ -32,6 +32,7 @@ OPT_DAC_WIDE_MIN = 11
 OPT_ATTNBLK_SPREAD = 12
 OPT_DAC_STAGE = 13
 OPT_DAC_STAGE_MIN = 14
+OPT_SCAN_PQ = 15
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
@@ -169,6 +170,8 @@ _SIGS = {
                                      c_void_p, c_void_p]),
     "zmi_mamba2_step": (c_int, [ctypes.POINTER(Mamba2Args), c_void_p]),
     "zmi_mamba2_scan": (c_int, [ctypes.POINTER(Mamba2Args), c_int, c_void_p]),
+    "zmi_mamba2_scan_ws": (c_int, [ctypes.POINTER(Mamba2Args), c_int, c_void_p, ctypes.c_int64, c_void_p]),
+    "zmi_mamba2_scan_ws_bytes": (ctypes.c_int64, [c_int, c_int, c_int]),
     "zmi_add_layernorm": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                   c_void_p, c_int, c_int, c_void_p]),
     "zmi_mamba_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(Mamba2Args), c_void_p, c_void_p, c_void_p]),

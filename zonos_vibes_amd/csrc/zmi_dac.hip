@@ -46,9 +46,9 @@ __device__ __forceinline__ float snake(float y, float a, float inv_a) {
 
 #ifdef ZMI_DAC_STAMPS
 // diagnostic builds only (tools/dac_stamps.py): per workgroup of the conv_stage_kernel launches with c_out ==
-// ZMI_DAC_STAMPS and tap_step == 1, thread 0 stores s_memrealtime stamps: [0] start, for stage s < 8:
-// [1 + 3 s] its loads landed (after its barrier), [2 + 3 s] the next stage's loads issued, [3 + 3 s] its MFMAs
-// issued; [30] all MFMAs done, [31] epilogue done
+// ZMI_DAC_STAMPS and tap_step == 1, thread 0 stores s_memrealtime stamps: [0] start, for stage s < 8: [1 + 3 s]
+// its loads landed (after its barrier), [2 + 3 s] = [1 + 3 s] (the next stage's loads are issued inside the MFMA
+// groups), [3 + 3 s] its MFMAs issued; [30] all MFMAs done, [31] epilogue done
 __device__ unsigned long long g_dac_stamps[8192][32];
 extern "C" int zmi_dac_stamps_read(void* dst, size_t bytes) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dac_stamps), bytes) == hipSuccess ? 0 : -1;
@@ -410,9 +410,6 @@ __global__ __launch_bounds__(512) void conv_stage_kernel(const ConvArgs a) {
   const int omin = in_off + min(0, (TAPS - 1) * a.tap_step);
   const int nbp = (BN + span + 15) / 16;
   const int nstages = a.c_in / (32 * CG);
-#ifndef ZMI_DAC_PROBE
-#define ZMI_DAC_PROBE 0  // diagnostic builds only (tools/build_variant.sh -DZMI_DAC_PROBE=n; WRONG results): 1 no MFMAs,
-#endif                   // 2 no loads after stage 0
   // per-lane LDS-DMA sources: the weight piece (g, tap, p) of stage s is 1 KiB at a_src + ((tap nci + s CG + g) c_out
   // + 16 p) 32 halfs (channel-blocked weights); halo piece (g, p) rows q_blk + omin + 16 p + prow
   const int nci = a.c_in / 32;
@@ -456,18 +453,9 @@ __global__ __launch_bounds__(512) void conv_stage_kernel(const ConvArgs a) {
     asm volatile("" ::: "memory");
     if (s < 8) ZMI_DSTAMP(1 + 3 * s);
     // every wave is done with stage s - 1, whose buffer stage s + 1 fills during this stage
-    const bool more = s + 1 < nstages && !(ZMI_DAC_PROBE == 2);
+    const bool more = s + 1 < nstages;
     const char* const buf = lds_raw + (s & 1) * STAGE;
     if (s < 8) ZMI_DSTAMP(2 + 3 * s);
-    if (ZMI_DAC_PROBE == 1) {
-      if (more) {
-        issue_halo(s + 1);
-#pragma unroll
-        for (int k = 0; k < KA; ++k)
-          if (wave + NW * k < NA) issue_a(s + 1, wave + NW * k);
-      }
-      continue;
-    }
     // the stage's (channel step, tap) MFMA groups with their fragments one group ahead in registers: the reads of
     // group u + 1 are issued before group u's MFMAs (a scheduling barrier keeps them there), so each group's 4-7
     // LDS reads have the previous group's 12-16 MFMAs to land in instead of stalling the wave

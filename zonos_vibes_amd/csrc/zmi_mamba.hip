@@ -123,6 +123,192 @@ __global__ __launch_bounds__(MB_NT) void mamba2_scan_kernel(const ZmiMamba2Args 
   }
 }
 
+// ---------------------------------------------------------------------------- parallel prefill scan
+// zmi_mamba2_scan_ws: the same Mamba2.forward from an empty state in two launches.
+//  (1) mamba2_conv_kernel, one workgroup per row: causal conv + SiLU of every xBC channel (conv4, bf16-rounded as
+//      the reference's conv output tensor) into the workspace, dt = softplus(dt + dt_bias) and dA = exp(A dt) per
+//      head, and, on each sequence's last row, the conv ring's four slots (the last raw inputs, zero below 0).
+//  (2) mamba2_scan2_kernel, one workgroup per (sequence, head, quarter of the 64 head dims): thread (p, n-block)
+//      owns state[p][8 n-block .. + 7] in fp32 registers and walks the positions in order,
+//          s = fma(s, dA, (B dt) x),   y_p = sum_n fma(s, C) (+ x D),
+//      the 16 n-blocks of a row summed by DPP (each block's 8 terms as two interleaved chains). The (sequence, head) recurrence the single-workgroup kernel runs on
+//      256 threads is spread over 1,024 (4x the workgroups, a quarter of each thread's state and FMA chain), and
+//      the conv no longer sits inside it. Its arithmetic differs from mamba2_scan_kernel's in fp32 rounding (fused
+//      multiply-adds, the readout summed over 8-wide blocks): both are checked against the oracle's recurrence.
+constexpr int S2_NB = MB_DS / 8;        // 16 n-blocks of 8 state columns
+constexpr int S2_TT = 32;               // positions staged per tile
+
+__global__ __launch_bounds__(256) void mamba2_conv_kernel(const ZmiMamba2Args a, int seq_len, bf16_t* xc, float* dts,
+                                                          float* das) {
+  // one thread per (row, channel): grid (rows, channel blocks of 256), every load of the launch in flight at once
+  const int row = blockIdx.x, sq = row / seq_len, q = row - sq * seq_len, row0 = sq * seq_len;
+  const int conv_dim = a.d_ssm + 2 * MB_DS, c = blockIdx.y * 256 + threadIdx.x;
+  const bf16_t* zx0 = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)row0 * a.ld_zx + a.d_ssm;
+  if (c < conv_dim) {
+    const bf16_t* cw = reinterpret_cast<const bf16_t*>(a.conv_w);
+    const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
+    float r[MB_DC];
+#pragma unroll
+    for (int k = 0; k < MB_DC; ++k) {
+      const int qq = q - (MB_DC - 1) + k;
+      r[k] = qq >= 0 ? bf2f(zx0[(size_t)qq * a.ld_zx + c]) : 0.f;
+    }
+    xc[(size_t)row * conv_dim + c] = (bf16_t)f2bf(conv4(cw + (size_t)c * MB_DC, bf2f(cb[c]), r[0], r[1], r[2], r[3]));
+    if (q == seq_len - 1) {  // the conv ring: slot qq % 4 holds the raw input of qq, for the last d_conv positions
+      const int kv = a.row_kv ? a.row_kv[row0] : sq;
+      bf16_t* ring = reinterpret_cast<bf16_t*>(a.conv_ring) + (size_t)kv * MB_DC * conv_dim;
+#pragma unroll
+      for (int k = 0; k < MB_DC; ++k) {
+        const int qq = seq_len - MB_DC + k;
+        ring[(size_t)(qq & 3) * conv_dim + c] = qq >= 0 ? zx0[(size_t)qq * a.ld_zx + c] : (bf16_t)0;
+      }
+    }
+  }
+  if (blockIdx.y == 0)
+    for (int h = threadIdx.x; h < a.nheads; h += 256) {
+      const float dtv = softplus_f(bf2f(zx0[(size_t)q * a.ld_zx + a.d_ssm + 2 * MB_DS + h]) + a.dt_bias[h]);
+      dts[(size_t)row * a.nheads + h] = dtv;
+      das[(size_t)row * a.nheads + h] = expf(a.A[h] * dtv);
+    }
+}
+
+// PQ workgroups per (sequence, head), each 64 / PQ head dims; thread (p-group, n-block) owns PR = 4 / PQ rows p
+// x 8 state columns, so each B / C value it reads from LDS serves PR rows
+#ifdef ZMI_SCAN_STAMPS
+// diagnostic builds only (tools/scan_probe.py --stamps): thread 0 of each workgroup stores s_memtime at the start,
+// and per tile k < 12 after its operands are in LDS [1 + 2k] and after its positions [2 + 2k]
+__device__ unsigned long long g_scan_stamps[1024][32];
+extern "C" int zmi_scan_stamps_read(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_scan_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#define ZMI_SSTAMP(i_)                                                                      \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_scan_stamps[blockIdx.x][i_] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define ZMI_SSTAMP(i_) \
+  do {                 \
+  } while (0)
+#endif
+
+template <int PQ>
+__global__ __launch_bounds__(256) void mamba2_scan2_kernel(const ZmiMamba2Args a, int seq_len, const bf16_t* xc,
+                                                           const float* dts, const float* das) {
+  constexpr int PW = MB_HD / PQ, PR = PW / 16;  // head dims per workgroup, rows per thread
+  const int pq = blockIdx.x % PQ, sh = blockIdx.x / PQ, h = sh % a.nheads, sq = sh / a.nheads;
+  const int row0 = sq * seq_len, conv_dim = a.d_ssm + 2 * MB_DS;
+  const int kv = a.row_kv ? a.row_kv[row0] : sq;
+  const int t = threadIdx.x, pg = t / S2_NB, nb = t % S2_NB, p0 = pq * PW + pg * PR;
+  __shared__ float xs[S2_TT][PW], bdt[S2_TT][MB_DS], cs[S2_TT][MB_DS], dA[S2_TT];
+  const float Dh = a.D[h];
+  // a tile's operands, one thread's share: (B dt, C) of (position tt = (t + 256 i) / 128, state column
+  // (t + 256 i) % 128) for i < 16, x of (t + 256 i) / PW, % PW, dA of position t; loaded into registers one
+  // tile ahead so their latency hides under the previous tile's recurrence
+  constexpr int NBC = S2_TT * MB_DS / 256, NX = S2_TT * PW / 256;
+  float rb[NBC], rc[NBC], rx[NX], rd = 0.f;
+  auto load = [&](int t0) {
+    const int nt = min(S2_TT, seq_len - t0);
+#pragma unroll
+    for (int i = 0; i < NBC; ++i) {
+      const int idx = t + 256 * i, tt = idx / MB_DS, n = idx - tt * MB_DS;
+      if (tt < nt) {
+        const size_t r = (size_t)(row0 + t0 + tt);
+        rb[i] = bf2f(xc[r * conv_dim + a.d_ssm + n]) * dts[r * a.nheads + h];
+        rc[i] = bf2f(xc[r * conv_dim + a.d_ssm + MB_DS + n]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int idx = t + 256 * i, tt = idx / PW, j = idx - tt * PW;
+      if (tt < nt) rx[i] = bf2f(xc[(size_t)(row0 + t0 + tt) * conv_dim + h * MB_HD + pq * PW + j]);
+    }
+    if (t < nt) rd = das[(size_t)(row0 + t0 + t) * a.nheads + h];
+  };
+  float st[PR][8];
+#pragma unroll
+  for (int r = 0; r < PR; ++r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[r][k] = 0.f;
+  bf16_t* y = reinterpret_cast<bf16_t*>(a.y);
+  ZMI_SSTAMP(0);
+  load(0);
+  for (int t0 = 0; t0 < seq_len; t0 += S2_TT) {
+    const int nt = min(S2_TT, seq_len - t0);
+    __syncthreads();  // the previous tile's readers are done
+#pragma unroll
+    for (int i = 0; i < NBC; ++i) {
+      const int idx = t + 256 * i, tt = idx / MB_DS, n = idx - tt * MB_DS;
+      bdt[tt][n] = rb[i];
+      cs[tt][n] = rc[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int idx = t + 256 * i;
+      xs[idx / PW][idx % PW] = rx[i];
+    }
+    if (t < S2_TT) dA[t] = rd;
+    __syncthreads();
+    if (t0 / S2_TT < 12) ZMI_SSTAMP(1 + 2 * (t0 / S2_TT));
+    if (t0 + S2_TT < seq_len) load(t0 + S2_TT);
+    // positions in groups of 4 with their stores behind one branch at the end: a position's readout (FMA
+    // chains, DPP sums) is off the state's critical path, so the next positions' LDS reads and state updates
+    // issue under it
+    auto step = [&](int tt, float (&v)[PR]) {
+      const float d = dA[tt];
+      const float4 b0 = *reinterpret_cast<const float4*>(&bdt[tt][nb * 8]);
+      const float4 b1 = *reinterpret_cast<const float4*>(&bdt[tt][nb * 8 + 4]);
+      const float4 c0 = *reinterpret_cast<const float4*>(&cs[tt][nb * 8]);
+      const float4 c1 = *reinterpret_cast<const float4*>(&cs[tt][nb * 8 + 4]);
+      const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int r = 0; r < PR; ++r) {
+        const float x = xs[tt][pg * PR + r];
+        float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          st[r][k] = fmaf(st[r][k], d, b[k] * x);
+          st[r][k + 1] = fmaf(st[r][k + 1], d, b[k + 1] * x);
+          o0 = fmaf(st[r][k], c[k], o0);
+          o1 = fmaf(st[r][k + 1], c[k + 1], o1);
+        }
+        v[r] = row16_sum(o0 + o1) + x * Dh;  // the 16 n-blocks of row p: 16 consecutive lanes
+      }
+    };
+    bf16_t* yp = y + (size_t)(row0 + t0) * a.ldy + h * MB_HD + p0;
+    int tt = 0;
+    for (; tt + 4 <= nt; tt += 4) {
+      float v[4][PR];
+      step(tt, v[0]);
+      step(tt + 1, v[1]);
+      step(tt + 2, v[2]);
+      step(tt + 3, v[3]);
+      if (nb == 0)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < PR; ++r) yp[(size_t)(tt + u) * a.ldy + r] = (bf16_t)f2bf(v[u][r]);
+    }
+    for (; tt < nt; ++tt) {
+      float v[PR];
+      step(tt, v);
+      if (nb == 0)
+#pragma unroll
+        for (int r = 0; r < PR; ++r) yp[(size_t)tt * a.ldy + r] = (bf16_t)f2bf(v[r]);
+    }
+    if (t0 / S2_TT < 12) ZMI_SSTAMP(2 + 2 * (t0 / S2_TT));
+  }
+  // final state, bf16 (the cache dtype): 8 consecutive n per row
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    bf16_t* sp = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p0 + r) * MB_DS + nb * 8;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = f2bf(st[r][2 * e]) | (f2bf(st[r][2 * e + 1]) << 16);
+    *reinterpret_cast<uint4*>(sp) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 // Row reductions of the two norms below: one 256-thread workgroup per row; the row is cut into NW
 // contiguous parts (4, or K / 512 below K = 2048), wave w < NW owns part w, lane L its 8-element chunks
 // L + 64 i; fp32 sums in chunk order, DPP wave sums, parts combined as (p0 + p1) + (p2 + p3) (absent parts
@@ -279,6 +465,44 @@ extern "C" int zmi_mamba2_scan(const ZmiMamba2Args* a, int seq_len, void* stream
   if (seq_len <= 0 || a->M % seq_len) return zmi_fail_msg("mamba2_scan: M must be a multiple of seq_len > 0");
   hipLaunchKernelGGL(mamba2_scan_kernel, dim3((unsigned)(a->M / seq_len * a->nheads)), dim3(MB_NT), 0,
                      (hipStream_t)stream, *a, seq_len);
+  ZMI_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int64_t zmi_mamba2_scan_ws_bytes(int m, int d_ssm, int nheads) {
+  if (m <= 0 || d_ssm <= 0 || nheads <= 0) return 0;
+  const int64_t xc = ((int64_t)m * (d_ssm + 2 * MB_DS) * 2 + 255) / 256 * 256;
+  return xc + 2 * (((int64_t)m * nheads * 4 + 255) / 256 * 256);
+}
+
+extern "C" int zmi_mamba2_scan_ws(const ZmiMamba2Args* a, int seq_len, void* ws, int64_t ws_bytes, void* stream) {
+  if (int e = check_mamba(a)) return e;
+  if (seq_len <= 0 || a->M % seq_len) return zmi_fail_msg("mamba2_scan_ws: M must be a multiple of seq_len > 0");
+  if (!ws || ws_bytes < zmi_mamba2_scan_ws_bytes(a->M, a->d_ssm, a->nheads))
+    return zmi_fail_msg("mamba2_scan_ws: workspace smaller than zmi_mamba2_scan_ws_bytes");
+  const int64_t xcb = ((int64_t)a->M * (a->d_ssm + 2 * MB_DS) * 2 + 255) / 256 * 256;
+  const int64_t hb = ((int64_t)a->M * a->nheads * 4 + 255) / 256 * 256;
+  bf16_t* xc = (bf16_t*)ws;
+  float* dts = (float*)((char*)ws + xcb);
+  float* das = (float*)((char*)ws + xcb + hb);
+  hipStream_t s = (hipStream_t)stream;
+  const int conv_dim = a->d_ssm + 2 * MB_DS;
+  hipLaunchKernelGGL(mamba2_conv_kernel, dim3((unsigned)a->M, (unsigned)((conv_dim + 255) / 256)), dim3(256), 0, s, *a,
+                     seq_len, xc, dts, das);
+  ZMI_CHECK(hipGetLastError());
+  const int pq = zmi_option(ZMI_OPT_SCAN_PQ);
+  const dim3 grid((unsigned)(a->M / seq_len * a->nheads * pq));
+  if (pq == 1)
+    hipLaunchKernelGGL(mamba2_scan2_kernel<1>, grid, dim3(256), 0, s, *a, seq_len, (const bf16_t*)xc,
+                       (const float*)dts, (const float*)das);
+  else if (pq == 2)
+    hipLaunchKernelGGL(mamba2_scan2_kernel<2>, grid, dim3(256), 0, s, *a, seq_len, (const bf16_t*)xc,
+                       (const float*)dts, (const float*)das);
+  else if (pq == 4)
+    hipLaunchKernelGGL(mamba2_scan2_kernel<4>, grid, dim3(256), 0, s, *a, seq_len, (const bf16_t*)xc,
+                       (const float*)dts, (const float*)das);
+  else
+    return zmi_fail_msg("mamba2_scan_ws: ZMI_OPT_SCAN_PQ must be 1, 2 or 4");
   ZMI_CHECK(hipGetLastError());
   return 0;
 }

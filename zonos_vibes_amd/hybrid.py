@@ -10,7 +10,7 @@ hipGraph-captured decode loop, slots — is HipEngine's; this class only swaps t
   Mamba2 block   zmi_mamba_block: in_proj GEMV + the Mamba2 step (conv ring + SiLU + selective state
                  update) in one launch, granule hand-off (zmi_mamba2_step as its own launch above 16 rows)
                  -> out_proj GEMV with the GRMS prologue (RMSNormGated; prefill: zmi_gated_rmsnorm and
-                 zmi_mamba2_scan over the sequence)
+                 zmi_mamba2_scan_ws over the sequence)
   MHA block      QKV GEMV (non-interleaved rotary as interleaved pairs on permuted q / k rows, bf16
                  cos / sin as flash-attn caches them) -> attention kernel -> out_proj GEMV
   optional MLP   (add + LayerNorm) fc1 SwiGLU GEMV -> fc2 GEMV       (d_intermediate > 0)
@@ -114,6 +114,8 @@ class HybridEngine(HipEngine):
             self.conv_ring = z(nm, R, md["d_conv"], md["conv_dim"])
             self.ssm = z(nm, R, md["nheads"], md["headdim"], md["d_state"])
             self.mgran = z(nm, R, md["d_in_proj"] // 2, dt=torch.int64)  # zmi_mamba_block hand-off granules
+            ws = int(self.lib.zmi_mamba2_scan_ws_bytes(2 * P, md["d_ssm"], md["nheads"]))
+            self.scan_ws = z(ws, dt=torch.uint8)  # zmi_mamba2_scan_ws: conv output, dt, dA of the prefill rows
             self.rope = rope_table_neox(self.hd).to(dev)
         self.stream.synchronize()
 
@@ -249,9 +251,9 @@ class HybridEngine(HipEngine):
                 items.append(("call", self._call_step(self._mamba_args(lw, zx, yb, m, row_pos, None))))
             else:
                 a = self._mamba_args(lw, zx, yb, m, row_pos, row_kv)
-                lib, s = self.lib, self.sptr
-                items.append(("call", lambda a=a: _lib.check(lib.zmi_mamba2_scan(ctypes.byref(a), seq_len, s),
-                                                             "mamba2_scan")))
+                lib, s, wp, wn = self.lib, self.sptr, self.scan_ws.data_ptr(), self.scan_ws.numel()
+                items.append(("call", lambda a=a: _lib.check(lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, wp, wn,
+                                                                                    s), "mamba2_scan_ws")))
             items.append(("call", self._gnorm(lw, yb, zx, yn, m)))
             items.append(("gemv", self._gemv(lw["out"], yn, m, d, md["d_ssm"], _lib.EPI_STORE, hid, d)))
         if lw.get("ff"):
