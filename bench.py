@@ -107,7 +107,7 @@ def time_dominant_kernel(model, cond, reps: int = 3):
 
 # the committed FETCH_SIZE pass of each dominant-kernel candidate (tools/gpu.sh round)
 PMC_FILES = {"layer_engine_kernel<0>": "r04_pmc_engine_fetch.json",
-             "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": "r04_pmc_fc1_fetch.json"}
+             "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": "r05_pmc_fc1_fetch.json"}
 
 
 def _time_fused(e, items, gran, run, reps: int) -> float:
@@ -917,7 +917,7 @@ def main():
                                     "unit": "TFLOP/s", "frac": round(dac_tf / MFMA_PEAK_TFLOPS, 4),
                                     "flop_per_frame": DAC_FLOP_PER_FRAME, "frames": n_new,
                                     "ms": breakdown["dac_decode_ms"],
-                                    "mfma_busy_source": "profiles/r03c_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
+                                    "mfma_busy_source": "profiles/r05_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
             "c3_sharded": c3,
             "widened": widened,
             "end_of_batch_gather": gather,
