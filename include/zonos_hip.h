@@ -385,9 +385,10 @@ int zmi_version(void);
  *   ZMI_OPT_ATTNBLK_SPREAD (default 5): zmi_attn_block's workgroups reserve LDS so the launch spreads over the chip;
  *          bits 0-1 for the 8-chunk split / score-exchange / self forms, bits 2-3 for the 24-chunk split form:
  *          0 = no reserve, 1 = one workgroup per CU, 2 = at most two.
- *   ZMI_OPT_DAC_STAGE (default 13): DAC convs on the staged K loop (one barrier per 32-channel step x all taps, one
+ *   ZMI_OPT_DAC_STAGE (default 29): DAC convs on the staged K loop (one barrier per 32-channel step x all taps, one
  *          512-thread workgroup per CU); bit 0 the k7 convs, bit 1 the 1x1 convs, bit 2 the transposed convs,
- *          bit 3 512-row time tiles for the k7 convs (256 otherwise).
+ *          bit 3 512-row time tiles for the k7 convs where their grid is large enough (256 otherwise), bit 4 the
+ *          256-row forms with 4 dedicated loader waves (768 threads).
  *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups.
  *   ZMI_OPT_SCAN_PQ (default 4): zmi_mamba2_scan_ws workgroups per (sequence, head) (1, 2 or 4; each thread then
  *          owns 4 / PQ head dims x 8 state columns). */

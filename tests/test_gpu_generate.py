@@ -271,7 +271,8 @@ def test_dac_decode_c5_length_windows_bit_identical():
 def test_dac_wide_time_tiles_bit_identical(frames):
     """The DAC convs on 256-row time tiles (512-thread workgroups, ZMI_OPT_DAC_WIDE = 2), on 128-row tiles (0), the
     per-conv choice (1), and on the staged K loop (conv_stage_kernel: ZMI_OPT_DAC_STAGE bits for the k7 / 1x1 /
-    transposed convs and 512-row k7 tiles, forced onto every eligible conv with ZMI_OPT_DAC_STAGE_MIN = 1, and the
+    transposed convs, 512-row k7 tiles and the loader-wave form, forced onto every eligible conv with
+    ZMI_OPT_DAC_STAGE_MIN = 1, and the
     default) give the
     same bits, decode and the encoder's latents: a conv output's K order and MFMA chain do not depend on the tile
     or on how many K steps share a barrier."""
@@ -284,7 +285,7 @@ def test_dac_wide_time_tiles_bit_identical(frames):
     lib = _lib.lib()
     knobs = (_lib.OPT_DAC_WIDE, _lib.OPT_DAC_STAGE, _lib.OPT_DAC_STAGE_MIN)
     old = [lib.zmi_get_option(k) for k in knobs]
-    cases = [(0, 0, 256), (2, 0, 256), (1, 0, 256), (1, 7, 1), (1, 15, 1), (1, 9, 256), tuple(old)]
+    cases = [(0, 0, 256), (2, 0, 256), (1, 0, 256), (1, 7, 1), (1, 15, 1), (1, 9, 256), (1, 23, 1), tuple(old)]
     outs = {}
     try:
         for case in cases:

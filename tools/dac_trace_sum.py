@@ -8,7 +8,7 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Time
 agg = collections.OrderedDict()
 for r in rows:
     n = r['Kernel_Name']
-    if 'conv_kernel' not in n and 'conv_stage_kernel' not in n:
+    if not any(k in n for k in ('conv_kernel', 'conv_stage_kernel', 'conv_ldr_kernel')):
         continue
     i = n.index('conv_')
     key = (n[i:n.index('>', i) + 1], r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'])

@@ -89,6 +89,17 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds) {
                : "memory");
 }
 
+// glds16 with the destination as a wave-uniform LDS byte address (base + offset computed once per kernel: a
+// generic -> LDS pointer cast per piece made the compiler emit a null check on src_shared_base that gfx950 rejects)
+__device__ __forceinline__ void glds16_at(const void* gsrc, unsigned ldst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(ldst)
+               : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 12]
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
@@ -182,7 +193,7 @@ struct ConvEpiChan {
 template <int WM, int WN, int NWN, int PARTS>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4_t (&acc)[WM][WN], char* lds_raw, int wn,
                                               int am, int lane, int q_blk, int co_blk, int out_phase,
-                                              const ConvEpiChan<WM, 128 * NWN>& ch) {
+                                              const ConvEpiChan<WM, 128 * NWN>& ch, bool writer = true) {
   static_assert(NWN % PARTS == 0, "a part is whole wave columns");
   constexpr int BM = 32 * WM, BN = 16 * WN * NWN, TP = BM + 4, WPP = NWN / PARTS;
   constexpr int ROWS = BN / PARTS, RPT = ConvEpiChan<WM, 128 * NWN>::RPT;
@@ -191,7 +202,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4_t (
   const int co = co_blk + ch.c8 * 8;
 #pragma unroll
   for (int part = 0; part < PARTS; ++part) {
-    if (wn / WPP == part) {
+    if (writer && wn / WPP == part) {
       const int rb = (wn % WPP) * 16 * WN;
 #pragma unroll
       for (int i = 0; i < WM; ++i)
@@ -487,6 +498,109 @@ __global__ __launch_bounds__(512) void conv_stage_kernel(const ConvArgs a) {
   ZMI_DSTAMP(31);
 }
 
+// The staged K loop with dedicated loader waves (ZMI_OPT_DAC_STAGE bit 4): 8 MFMA waves (2 along the channels x 4
+// along 256 time rows, WN = 4) and 4 loader waves, one per SIMD. Only the loaders issue LDS-DMA, so an MFMA wave's
+// instruction stream holds nothing but fragment reads and MFMAs, and a loader stalled on the load path's
+// back-pressure stalls no MFMA: stage s + 1's pieces are issued right after the barrier that opens stage s and
+// land while its MFMAs run. Same stage buffers, K order and epilogue as conv_stage_kernel (bit-identical).
+template <int WM, int TAPS, int CG, int HROWS>
+__global__ __launch_bounds__(768) void conv_ldr_kernel(const ConvArgs a) {
+  constexpr int NWN = 4, WN = 4, NW = 8, NLD = 4;
+  constexpr int BM = 32 * WM, BN = 64 * WN, NPA = BM / 16;
+  constexpr int HP = (BN + HROWS + 15) / 16;
+  constexpr int NA = TAPS * CG * NPA;
+  constexpr int A_BYTES = NA * 1024, STAGE = A_BYTES + CG * HP * 1024;
+  constexpr int PARTS = BN * (BM + 4) * 4 <= 2 * STAGE ? 1 : 2, TILE_BYTES = BN / PARTS * (BM + 4) * 4;
+  constexpr int LDS_BYTES = 2 * STAGE > TILE_BYTES ? 2 * STAGE : TILE_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "stage buffers exceed the CU's LDS");
+  __shared__ __attribute__((aligned(1024))) char lds_raw[LDS_BYTES];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool loader = wave >= NW;
+  const int lw = wave - NW;
+  const int wm = (loader ? 0 : wave) / NWN, wn = (loader ? 0 : wave) % NWN;
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int co_blk = blockIdx.y * BM, q_blk = blockIdx.x * BN;
+  const int rho = blockIdx.z;
+  const f16_t* const wts = a.w + (size_t)rho * a.w_phase;
+  const int in_off = a.nphase > 1 ? (rho + a.phase_pad) / a.out_stride : a.in_off;
+  const int out_phase = a.nphase > 1 ? rho : a.out_phase;
+  const int prow = lane >> 2, pchunk = (lane & 3) ^ (((lane >> 4) & 1) << 1);
+  const int am = wm * (16 * WM), bn = wn * (16 * WN);
+  const int span = (TAPS - 1) * abs(a.tap_step);
+  const int omin = in_off + min(0, (TAPS - 1) * a.tap_step);
+  const int nbp = (BN + span + 15) / 16;
+  const int nstages = a.c_in / (32 * CG);
+  const int nci = a.c_in / 32;
+  const f16_t* const a_src = wts + (TAPS == 1 ? (size_t)(co_blk + prow) * a.c_in : (size_t)(co_blk + prow) * 32) +
+                             pchunk * 8;
+  const unsigned lbase =
+      __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_raw);
+  auto issue = [&](int s) {  // this loader's pieces of stage s: weight pieces lw, lw + 4, ..., then halo pieces
+    const unsigned buf = lbase + (unsigned)((s & 1) * STAGE);
+#pragma unroll
+    for (int k = 0; k < (NA + NLD - 1) / NLD; ++k) {
+      const int P = lw + NLD * k;
+      if (P < NA) {
+        const int g = P / (TAPS * NPA), r = P - g * (TAPS * NPA), tap = r / NPA, p = r - tap * NPA;
+        glds16_at(a_src + (TAPS == 1 ? (size_t)16 * p * a.c_in + (s * CG + g) * 32
+                                     : ((size_t)(tap * nci + s * CG + g) * a.c_out + 16 * p) * 32),
+                  buf + (unsigned)(P * 1024));
+      }
+    }
+    for (int P = lw; P < CG * nbp; P += NLD) {
+      const int g = CG == 1 ? 0 : P / nbp, p = P - g * nbp;
+      const int tin = q_blk + omin + 16 * p + prow;
+      const bool ok = tin >= 0 && tin < a.t_in;
+      glds16_at(ok ? (const void*)(a.x + (size_t)tin * a.c_in + (s * CG + g) * 32 + pchunk * 8)
+                   : (const void*)&g_conv_zero[lane & 3],
+                buf + (unsigned)(A_BYTES + (g * HP + p) * 1024));
+    }
+  };
+  if (loader) issue(0);
+  ConvEpiChan<WM, 512> ch;
+  ch.load(a, co_blk);
+  constexpr int G = CG * TAPS;
+  for (int s = 0; s < nstages; ++s) {
+    if (loader) wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // every wave is done with stage s - 1, whose buffer the loaders now fill with stage s + 1
+    if (loader) {
+      if (s + 1 < nstages) issue(s + 1);
+    } else {
+      const char* const buf = lds_raw + (s & 1) * STAGE;
+      if constexpr (WM >= 4) {  // 168 VGPRs (3 waves per SIMD): no room for a second fragment set
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const int g = u / TAPS, tap = u - g * TAPS;
+          conv_mfma<WM, WN>(acc, buf + u * NPA * 1024, buf + A_BYTES + g * HP * 1024, in_off + tap * a.tap_step - omin,
+                            am, bn, lane);
+        }
+      } else {
+        ConvFrag<WM, WN> fr[2];
+        conv_load(fr[0], buf, buf + A_BYTES, in_off - omin, am, bn, lane);
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          if (u + 1 < G) {
+            const int g = (u + 1) / TAPS, tap = (u + 1) - g * TAPS;
+            conv_load(fr[(u + 1) & 1], buf + (u + 1) * NPA * 1024, buf + A_BYTES + g * HP * 1024,
+                      in_off + tap * a.tap_step - omin, am, bn, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          conv_compute(acc, fr[u & 1]);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+  __syncthreads();
+  conv_epilogue<WM, WN, NWN, PARTS>(a, acc, lds_raw, wn, am, lane, q_blk, co_blk, out_phase, ch, !loader);
+}
+
 // quantizer.from_codes (modeling_dac.py:347-371): 9 x [codebook gather (8-d) -> 1x1 conv to 1024 + bias], summed
 __global__ __launch_bounds__(256) void from_codes_kernel(const int64_t* codes, int T, const float* cbooks,
                                                           const float* pw, const float* pb, f16_t* z) {
@@ -715,16 +829,29 @@ static int launch_stage(const ConvArgs& a, hipStream_t s) {
   if (!(mask >> cls & 1) || !cg || a.c_out < 64) return 1;
   // 512-row time tiles (WN = 8, bit 3) for the k7 convs: half the weight bytes per MFMA of the 256-row tile, at
   // most 96 channels per tile (LDS)
-  const bool wide = cls == 0 && (mask & 8);
-  const int bn = wide ? 512 : 256, wm_max = wide ? 3 : 4;
-  const unsigned nq = (unsigned)((a.n_out + bn - 1) / bn), nz = (unsigned)a.nphase;
-  int wm = 0;
-  for (int c : {4, 3, 2, 1})
-    if (c <= wm_max && a.c_out % (32 * c) == 0) {
-      wm = c;
-      if ((long)nq * nz * (a.c_out / (32 * c)) >= zmi_option(ZMI_OPT_DAC_STAGE_MIN)) break;
-    }
-  if (!wm || (long)nq * nz * (a.c_out / (32 * wm)) < zmi_option(ZMI_OPT_DAC_STAGE_MIN)) return 1;
+  // A grid with too few 512-row tiles (conv1 at 861 frames: 96) takes the 256-row tiles before conv_kernel (its 192
+  // workgroups: 40 us against 136 on conv_kernel).
+  const long min_wg = zmi_option(ZMI_OPT_DAC_STAGE_MIN);
+  const unsigned nz = (unsigned)a.nphase;
+  auto pick = [&](int bn, int wm_max, unsigned* nq_out) {  // the largest tile height whose grid reaches min_wg
+    const unsigned nq = (unsigned)((a.n_out + bn - 1) / bn);
+    int w = 0;
+    for (int c : {4, 3, 2, 1})
+      if (c <= wm_max && a.c_out % (32 * c) == 0) {
+        w = c;
+        if ((long)nq * nz * (a.c_out / (32 * c)) >= min_wg) break;
+      }
+    *nq_out = nq;
+    return w && (long)nq * nz * (a.c_out / (32 * w)) >= min_wg ? w : 0;
+  };
+  unsigned nq = 0;
+  bool wide = cls == 0 && (mask & 8);
+  int wm = wide ? pick(512, 3, &nq) : 0;
+  if (!wm) {
+    wide = false;
+    wm = pick(256, 4, &nq);
+  }
+  if (!wm) return 1;
   if (cls == 1 && cg == 3 && wm < 3) return 1;  // instantiated for the 96-channel stages only
   const dim3 grid(nq, (unsigned)(a.c_out / (32 * wm)), nz);
 #define ZMI_STAGE_L(wm_, wn_, taps_, cg_, hrows_) \
@@ -736,7 +863,26 @@ static int launch_stage(const ConvArgs& a, hipStream_t s) {
     case 2: ZMI_STAGE_L(2, wn_, taps_, cg_, hrows_); break;  \
     default: ZMI_STAGE_L(1, wn_, taps_, cg_, hrows_); break; \
   }
-  if (wide) {
+  if ((mask & 16) && !wide && (cls == 0 || cls == 2)) {
+#define ZMI_LDR_L(wm_, taps_, cg_, hrows_) \
+  hipLaunchKernelGGL((conv_ldr_kernel<wm_, taps_, cg_, hrows_>), grid, dim3(768), 0, s, a)
+    if (cls == 0) {
+      switch (wm) {
+        case 4: ZMI_LDR_L(4, 7, 1, 64); break;
+        case 3: ZMI_LDR_L(3, 7, 1, 64); break;
+        case 2: ZMI_LDR_L(2, 7, 1, 64); break;
+        default: ZMI_LDR_L(1, 7, 1, 64); break;
+      }
+    } else {
+      switch (wm) {
+        case 4: ZMI_LDR_L(4, 2, 2, 16); break;
+        case 3: ZMI_LDR_L(3, 2, 2, 16); break;
+        case 2: ZMI_LDR_L(2, 2, 2, 16); break;
+        default: ZMI_LDR_L(1, 2, 2, 16); break;
+      }
+    }
+#undef ZMI_LDR_L
+  } else if (wide) {
     switch (wm) {
       case 3: ZMI_STAGE_L(3, 8, 7, 1, 64); break;
       case 2: ZMI_STAGE_L(2, 8, 7, 1, 64); break;
