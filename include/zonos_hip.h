@@ -70,11 +70,13 @@ typedef struct ZmiGemvArgs {
 int zmi_pack_weight(const void* src, void* dst, int n_src, int k, int n_pad, int mode, void* stream);
 /* One kernel for every M: a row's result is bit-identical whatever the batch it is computed in. */
 int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream);
-/* Many-row fc2 (K = 8192) or out_proj (K = 2048), EPI_RESIDUAL, plain (reference _torch.py:100-101,141,152): a
- * split-K GEMM (one workgroup per 64-column block and K segment -- 8 x 1024 / 4 x 512, the GEMV's wave split --,
- * fp32 segment sums in `part`, then a reduce launch adding the segments in K order + the residual epilogue). Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment MFMA chains and segment
- * order); reads the activation rows once per column block instead of once per column group. part:
- * zmi_gemv_splitk_floats(M, N) floats. */
+/* Many-row fc2 (K = 8192) or out_proj (K = 2048), EPI_RESIDUAL, plain (reference _torch.py:100-101,141,152), or
+ * the hybrid's Mamba2 out_proj (K = 4096 = d_ssm, EPI_STORE: mamba_ssm out_proj of the prefill): a split-K GEMM
+ * (one workgroup per 64-column block, K segment -- 8 x 1024 / 4 x 1024 / 4 x 512, the GEMV's wave split -- and
+ * row group, ZMI_OPT_SPLITK_WGS), fp32 segment sums in `part`, then a reduce launch adding the segments in K
+ * order + the residual / store epilogue. Bit-identical to zmi_gemv_launch for every row (the GEMV's per-segment
+ * MFMA chains and segment order); reads the activation rows once per column block instead of once per column
+ * group. part: zmi_gemv_splitk_floats(M, N) floats. */
 int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream);
 /* The same with ln_w != NULL (N = 2048): the reduce also writes LayerNorm(new row; ln_w, ln_b, eps) to xn [M][ldxn],
  * bit-identical to zmi_layernorm_rows of the new rows, so the next op's LayerNorm pre-pass is not launched. */
@@ -391,11 +393,13 @@ int zmi_version(void);
  *          256-row forms with 4 dedicated loader waves (768 threads).
  *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups.
  *   ZMI_OPT_SCAN_PQ (default 4): zmi_mamba2_scan_ws workgroups per (sequence, head) (1, 2 or 4; each thread then
- *          owns 4 / PQ head dims x 8 state columns). */
+ *          owns 4 / PQ head dims x 8 state columns).
+ *   ZMI_OPT_SPLITK_WGS (default 256): zmi_gemv_splitk splits the rows into groups of 16-row tiles until its grid
+ *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
        ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
-       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_COUNT = 16 };
+       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_SPLITK_WGS = 16, ZMI_OPT_COUNT = 17 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

@@ -1,8 +1,8 @@
-"""The split-K fc2 / out_proj GEMM (zmi_gemv_splitk: one workgroup per 64-column block and K segment -- 8 x 1024
-for K = 8192, 4 x 512 for K = 2048 --, fp32 segment sums, a reduce launch adding them in K order + the residual
-epilogue) against zmi_gemv_launch's GEMV for the same EPI_RESIDUAL op: bit-identical for row counts on and off
-the 16-row tile and across the GEMV's own launch forms at those counts (a row's result may not depend on the
-batch it is computed in)."""
+"""The split-K fc2 / out_proj GEMM (zmi_gemv_splitk: one workgroup per 64-column block, K segment -- 8 x 1024
+for K = 8192, 4 x 1024 for the hybrid's K = 4096 Mamba2 out_proj, 4 x 512 for K = 2048 -- and row group, fp32
+segment sums, a reduce launch adding them in K order + the residual / store epilogue) against zmi_gemv_launch's
+GEMV for the same op: bit-identical for row counts on and off the 16-row tile, across the GEMV's own launch forms
+at those counts and across row groupings (a row's result may not depend on the batch it is computed in)."""
 import ctypes
 
 import pytest
@@ -15,10 +15,12 @@ pytestmark = pytest.mark.gpu
 D, F = 2048, 8192
 
 
-@pytest.mark.parametrize("K", [F, D])
+@pytest.mark.parametrize("wgs", [256, 0, 1024])
+@pytest.mark.parametrize("K", [F, 4096, D])
 @pytest.mark.parametrize("M", [1, 16, 17, 64, 65, 128, 322])
-def test_splitk_bit_identical_to_gemv(M, K):
+def test_splitk_bit_identical_to_gemv(M, K, wgs):
     L = _lib()
+    epi = L.EPI_STORE if K == 4096 else L.EPI_RESIDUAL
     W = rnd(D, K, scale=0.03, seed=70)
     Wp = pack(W)[0]
     h = rnd(M, K, scale=1.0, seed=71)
@@ -32,13 +34,18 @@ def test_splitk_bit_identical_to_gemv(M, K):
 
     ref = x0.clone()
     a = args(ref)
-    L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), L.EPI_RESIDUAL, stream_ptr()))
+    L.check(L.lib().zmi_gemv_launch(ctypes.byref(a), epi, stream_ptr()))
     got = x0.clone()
     nf = L.lib().zmi_gemv_splitk_floats(M, D)
     part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
     a = args(got)
-    L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), L.EPI_RESIDUAL, part.data_ptr(), nf, stream_ptr()), "splitk")
-    torch.cuda.synchronize()
+    old = L.lib().zmi_get_option(L.OPT_SPLITK_WGS)
+    L.lib().zmi_set_option(L.OPT_SPLITK_WGS, wgs)
+    try:
+        L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), epi, part.data_ptr(), nf, stream_ptr()), "splitk")
+        torch.cuda.synchronize()
+    finally:
+        L.lib().zmi_set_option(L.OPT_SPLITK_WGS, old)
     assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
 
 

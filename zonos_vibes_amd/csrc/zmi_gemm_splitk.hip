@@ -23,7 +23,8 @@ namespace {
 using zmi_gemv::dma_piece;
 using zmi_gemv::ror8;
 
-// K segments are the GEMV's wave segments: K = 8192 (fc2) W = 8 x 16 chunks, K = 2048 (out_proj) W = 4 x 8
+// K segments are the GEMV's wave segments: K = 8192 (fc2) W = 8 x 16 chunks, K = 4096 (the hybrid's Mamba2
+// out_proj over d_ssm) W = 4 x 16, K = 2048 (out_proj) W = 4 x 8 (zmi_gemv_impl.h shape_for)
 template <int K>
 struct Shape {
   static constexpr int NSEG = K == 8192 ? 8 : 4, KS = K / NSEG, NL = KS / 64, KC = K / 64;
@@ -33,18 +34,22 @@ struct Shape {
 constexpr int NWV = 8, NT = NWV * 64;  // wave g = column group cb * 8 + g
 constexpr int RT = 16;                 // rows per tile (one MFMA tile)
 
+// Grid: (row group, K segment, column block), column blocks fastest. A row group is `rpg` consecutive 16-row tiles
+// (several row groups re-read the segment's weights, from L2 when they run together; speed only: a row's sums
+// do not depend on the grouping).
 template <int K>
-__global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb) {
+__global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb, int rpg) {
   using S = Shape<K>;
   constexpr int NSEG = S::NSEG, KS = S::KS, NL = S::NL, KC = S::KC, SROW = S::SROW, TILE_BYTES = S::TILE_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x;
+  const int b = blockIdx.x % (n_cb * NSEG), rg = blockIdx.x / (n_cb * NSEG);
   const int seg = b / n_cb, cb = b - seg * n_cb;  // consecutive blocks: one segment, neighbouring columns
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int g = cb * NWV + wave;
   const int M = a.M, N = a.N;
-  const int n_rt = (M + RT - 1) / RT;
+  const int rt0 = rg * rpg, n_rt = min((M + RT - 1) / RT, rt0 + rpg);
+  if (rt0 >= n_rt) return;
   bf16_t* tiles = reinterpret_cast<bf16_t*>(smem);  // two tile buffers
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)seg * KS;
 
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
       dma_piece(X + (size_t)(row0 + r) * a.ldx + p * 512 + lane * 8, dst + r * SROW + p * 512);
     }
   };
-  stage(0, 0);
+  stage(rt0, 0);
   // the wave's weights for this segment: group g, chunks seg * 16 .. + 15 (layout M8), all in flight
   const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)g * KC + seg * NL) * 1024;
   const __amdgpu_buffer_rsrc_t wrsrc =
@@ -65,11 +70,11 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
 #pragma unroll
   for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, 2);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // the first tile's pieces (issued before)
-  for (int rt = 0; rt < n_rt; ++rt) {
+  for (int rt = rt0; rt < n_rt; ++rt) {
     __syncthreads();  // tile rt landed for every wave's pieces; buffer rt + 1 is free
-    if (rt + 1 < n_rt) stage(rt + 1, (rt + 1) & 1);
+    if (rt + 1 < n_rt) stage(rt + 1, (rt + 1 - rt0) & 1);
     const int row0 = rt * RT, rows = min(RT, M - row0);
-    const bf16_t* xs = tiles + (size_t)(rt & 1) * (TILE_BYTES / 2);
+    const bf16_t* xs = tiles + (size_t)((rt - rt0) & 1) * (TILE_BYTES / 2);
     f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int ar = min(lane & 15, rows - 1);
     const bf16_t* xa = xs + ar * SROW + (lane >> 4) * 8;
@@ -93,8 +98,9 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
   }
 }
 
-// x[m][n] = bf16(x + bf16(sum over the segments in order)), the GEMV's EPI_RESIDUAL epilogue
-template <int NSEG>
+// x[m][n] = bf16(x + bf16(sum over the segments in order)), the GEMV's EPI_RESIDUAL epilogue; RES false: out = bf16(sum),
+// its EPI_STORE epilogue
+template <int NSEG, bool RES>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, int M, int N, bf16_t* out, int ldo) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (size_t)M * N) return;
@@ -103,7 +109,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* part, i
 #pragma unroll
   for (int s = 1; s < NSEG; ++s) v += part[(size_t)s * M * N + i];
   bf16_t* o = out + m * ldo + n;
-  *o = (bf16_t)f2bf(bf2f(*o) + bfround(v));
+  if (RES)
+    *o = (bf16_t)f2bf(bf2f(*o) + bfround(v));
+  else
+    *o = (bf16_t)f2bf(v);
 }
 
 // The same reduce + residual for rows of 2048 columns, then the LayerNorm of each new row into `xn` (the next
@@ -161,23 +170,32 @@ extern "C" int64_t zmi_gemv_splitk_floats(int M, int N) { return M <= 0 || N <= 
 
 namespace {
 template <int K>
-int launch_splitk(const ZmiGemvArgs& a, float* part, const void* ln_w, const void* ln_b, float eps, void* xn, int ldxn,
-                  hipStream_t s) {
+int launch_splitk(const ZmiGemvArgs& a, int epi, float* part, const void* ln_w, const void* ln_b, float eps, void* xn,
+                  int ldxn, hipStream_t s) {
   using S = Shape<K>;
   const int n_cb = a.N / (8 * NWV);
+  // row groups: about ZMI_OPT_SPLITK_WGS workgroups in all (0: one row group)
+  const int n_rt = (a.M + RT - 1) / RT, target = zmi_option(ZMI_OPT_SPLITK_WGS);
+  const int n_rg = std::max(1, std::min(n_rt, target / (n_cb * S::NSEG)));
+  const int rpg = (n_rt + n_rg - 1) / n_rg;
   const size_t lds = 2 * (size_t)S::TILE_BYTES;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   ZMI_CHECK(attr);
-  hipLaunchKernelGGL(splitk_kernel<K>, dim3(n_cb * S::NSEG), dim3(NT), lds, s, a, part, n_cb);
+  hipLaunchKernelGGL(splitk_kernel<K>, dim3(n_cb * S::NSEG * ((n_rt + rpg - 1) / rpg)), dim3(NT), lds, s, a, part,
+                     n_cb, rpg);
   ZMI_CHECK(hipGetLastError());
   if (ln_w) {
     hipLaunchKernelGGL(splitk_reduce_ln_kernel<S::NSEG>, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,
                        (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, (bf16_t*)xn, ldxn);
   } else {
     const size_t total = (size_t)a.M * a.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel<S::NSEG>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, part, a.M,
-                       a.N, (bf16_t*)a.out, a.ldo);
+    if (epi == ZMI_EPI_RESIDUAL)
+      hipLaunchKernelGGL((splitk_reduce_kernel<S::NSEG, true>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                         part, a.M, a.N, (bf16_t*)a.out, a.ldo);
+    else
+      hipLaunchKernelGGL((splitk_reduce_kernel<S::NSEG, false>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                         part, a.M, a.N, (bf16_t*)a.out, a.ldo);
   }
   ZMI_CHECK(hipGetLastError());
   return 0;
@@ -189,16 +207,18 @@ extern "C" int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part,
   const ZmiGemvArgs& a = *args;
   if (ln_w && (!ln_b || !xn || a.N != 2048 || ldxn < 2048 || ldxn % 8 || a.ldo % 8))
     return zmi_fail_msg("gemv_splitk_ln: the fused LayerNorm needs N = 2048, ln_b, xn (ldxn % 8) and ldo % 8");
-  if (epi != ZMI_EPI_RESIDUAL) return zmi_fail_msg("gemv_splitk: EPI_RESIDUAL only");
-  if ((a.K != 8192 && a.K != 2048) || a.ln_w || a.pro != ZMI_PRO_AUTO)
-    return zmi_fail_msg("gemv_splitk: plain K = 8192 (fc2) or 2048 (out_proj) only");
+  if (epi != ZMI_EPI_RESIDUAL && epi != ZMI_EPI_STORE) return zmi_fail_msg("gemv_splitk: EPI_RESIDUAL or EPI_STORE only");
+  if (ln_w && epi != ZMI_EPI_RESIDUAL) return zmi_fail_msg("gemv_splitk_ln: the fused LayerNorm follows EPI_RESIDUAL");
+  if ((a.K != 8192 && a.K != 4096 && a.K != 2048) || a.ln_w || a.pro != ZMI_PRO_AUTO)
+    return zmi_fail_msg("gemv_splitk: plain K = 8192 (fc2), 4096 (Mamba2 out_proj) or 2048 (out_proj) only");
   if (a.N % (8 * NWV) || a.n_valid != a.N) return zmi_fail_msg("gemv_splitk: N a multiple of 64, unpadded");
   if (a.M < 1 || a.ldx % 8 || a.ldo < a.N) return zmi_fail_msg("gemv_splitk: rows / strides");
-  const int nseg = a.K == 8192 ? Shape<8192>::NSEG : Shape<2048>::NSEG;
+  const int nseg = a.K == 8192 ? Shape<8192>::NSEG : (a.K == 4096 ? Shape<4096>::NSEG : Shape<2048>::NSEG);
   if (!part || part_floats < (int64_t)nseg * a.M * a.N) return zmi_fail_msg("gemv_splitk: partial buffer too small");
   hipStream_t s = (hipStream_t)stream;
-  return a.K == 8192 ? launch_splitk<8192>(a, part, ln_w, ln_b, eps, xn, ldxn, s)
-                     : launch_splitk<2048>(a, part, ln_w, ln_b, eps, xn, ldxn, s);
+  if (a.K == 8192) return launch_splitk<8192>(a, epi, part, ln_w, ln_b, eps, xn, ldxn, s);
+  if (a.K == 4096) return launch_splitk<4096>(a, epi, part, ln_w, ln_b, eps, xn, ldxn, s);
+  return launch_splitk<2048>(a, epi, part, ln_w, ln_b, eps, xn, ldxn, s);
 }
 
 extern "C" int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, void* stream) {

@@ -173,6 +173,9 @@ class HipEngine:
         self.layer_engine = False
         self.splitk_rows = 16
         self.splitk_o_rows = 16
+        # the hybrid's Mamba2 out_proj (K = d_ssm = 4096, EPI_STORE) over >= `splitk_m_rows` rows (its prefill: the
+        # GEMV form re-read every row's 8 KB activation row per 8-column group, 67 us at 322 rows)
+        self.splitk_m_rows = 16
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
@@ -345,8 +348,9 @@ class HipEngine:
         _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
 
     def _use_splitk(self, a, epi) -> bool:
-        lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows}.get(a.K, 0)
-        return (lo > 0 and a.M >= lo and epi == _lib.EPI_RESIDUAL and not a.ln_w and a.pro == _lib.PRO_AUTO
+        lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows, 4096: self.splitk_m_rows}.get(a.K, 0)
+        want = _lib.EPI_STORE if a.K == 4096 else _lib.EPI_RESIDUAL  # 4096: the hybrid's Mamba2 out_proj (d_ssm)
+        return (lo > 0 and a.M >= lo and epi == want and not a.ln_w and a.pro == _lib.PRO_AUTO
                 and a.N % 64 == 0 and a.n_valid == a.N
                 and a.M * a.N * (8 if a.K == 8192 else 4) <= self.splitk_part.numel())
 
