@@ -366,9 +366,10 @@ int zmi_version(void);
 /* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
  *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the
  *   dispatcher spreads their workgroups evenly over the CUs instead of packing several onto one CU.
- *   ZMI_OPT_GEMM_ROWS (default 1): plain K = 2048 GEMVs over many rows run the many-row form (64 columns per
+ *   ZMI_OPT_GEMM_ROWS (default 3): plain K = 2048 GEMVs over many rows run the many-row form (64 columns per
  *   workgroup, activation tiles DMA'd two ahead, one barrier per tile) where it measured faster than the
- *   32-column tile loop; 0 = always the tile loop.
+ *   32-column tile loop; 0 = always the tile loop; bit 1: the dense-pair MFMA forms of the many-row form and of
+ *   zmi_gemv_splitk (16 real columns per MFMA instead of 8, same bits; 1 = the M8 forms).
  *   ZMI_OPT_AF_DEPTH (default 3): weight loads each streaming wave of zmi_attn_ffn_block keeps in flight (1 KiB
  *          each; 2, 3, 4, 6 or 0 = unthrottled): the launch's latency-bound hand-offs queue behind whatever the
  *          chip has in flight, so the weight stream is issued progressively.

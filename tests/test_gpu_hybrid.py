@@ -122,12 +122,16 @@ def test_mamba2_step_matches_oracle():
             assert torch.equal(dev["ring"][r, (p - k) & 3].cpu(), ring[r, (p - k) & 3])
 
 
-@pytest.mark.parametrize("form", ["scan", "scan_ws"])
-@pytest.mark.parametrize("seq_len", [1, 3, 45, 161])
+@pytest.mark.parametrize("form", ["scan", "scan_ws", "scan_ssd"])
+@pytest.mark.parametrize("seq_len", [1, 3, 45, 161, 256, 257])
 def test_mamba2_scan_matches_oracle(seq_len, form):
     """Mamba2.forward from an empty cache for two sequences (tile edges at 32 positions; 161 = C4's prefill), by the
-    single-workgroup scan (zmi_mamba2_scan) and the parallel form the engine runs (zmi_mamba2_scan_ws: conv launch
-    + 4 workgroups per (sequence, head), fused multiply-adds): y within 4 bf16 ulps, the final state within 1."""
+    single-workgroup scan (zmi_mamba2_scan), the parallel form (zmi_mamba2_scan_ws: conv launch + 4 workgroups per
+    (sequence, head), fused multiply-adds) and the quadratic SSD form (scan_ws with ZMI_OPT_SCAN_PQ = 0: MFMA tiles of
+    C B^T, the decay matrix and the state sum; sequences past 256 positions fall back to the 4-workgroup scan): y
+    within 4 bf16 ulps, the final state within 1."""
+    if seq_len > 161 and form == "scan":
+        pytest.skip("the single-workgroup scan is covered to 161")
     L, lib = _lib()
     md = tiny_hybrid().backbone.mamba2_dims()
     cw, cb, dtb, A, D = _mamba_params(md, 21)
@@ -145,8 +149,13 @@ def test_mamba2_scan_matches_oracle(seq_len, form):
     else:
         nb = int(lib.zmi_mamba2_scan_ws_bytes(2 * seq_len, md["d_ssm"], md["nheads"]))
         ws = torch.full((nb,), 0xA5, dtype=torch.uint8, device=DEV)  # stale workspace must not matter
-        L.check(lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb, 0), "scan_ws")
-        assert lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb - 1, 0) != 0  # too small: refused
+        old = lib.zmi_get_option(L.OPT_SCAN_PQ)
+        lib.zmi_set_option(L.OPT_SCAN_PQ, 0 if form == "scan_ssd" else 4)
+        try:
+            L.check(lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb, 0), form)
+            assert lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb - 1, 0) != 0  # too small: refused
+        finally:
+            lib.zmi_set_option(L.OPT_SCAN_PQ, old)
     torch.cuda.synchronize()
     ry, rs, rconv = mamba2_scan_ref(zx, cw, cb, dtb, A, D, md)
     assert _ulps(y.view(2, seq_len, -1), ry) <= 4.0

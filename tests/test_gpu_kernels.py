@@ -97,16 +97,27 @@ PROD_SHAPES = {  # Zonos-v0.1 decode GEMVs: (N, K, LayerNorm'd, epilogue, pack m
     "fc2_residual": (2048, 8192, False, "residual", 0)}
 
 
+@pytest.mark.parametrize("rows_opt", [1, 3])
 @pytest.mark.parametrize("name", list(PROD_SHAPES))
-def test_gemv_batch_invariant_production_shapes(name):
+def test_gemv_batch_invariant_production_shapes(name, rows_opt):
     """The many-row GEMV geometries (the K = 2048 many-row form with its tiles DMA'd two ahead, or the
     4-column-group tile loop, by row count and width; per-shape workgroup targets) give every row the bits
     of the decode-step launch (1-16 rows, single tile, LayerNorm prologue) at the production shapes,
     epilogues included; the many-row plan LayerNorms its rows once per layer (zmi_layernorm_rows), the
     decode plan in the GEMV prologue: generate_batch == generate rests on exactly this. The row ranges
-    cross the many-row form's selection bounds (32, 64 rows)."""
-    from zonos_vibes_amd.engine import rope_table
+    cross the many-row form's selection bounds (32, 64 rows). rows_opt 3: the many-row form's dense-pair MFMAs
+    (ZMI_OPT_GEMM_ROWS bit 1)."""
     L = _lib()
+    old = L.lib().zmi_get_option(L.OPT_GEMM_ROWS)
+    L.lib().zmi_set_option(L.OPT_GEMM_ROWS, rows_opt)
+    try:
+        _batch_invariant_production_shape(L, name)
+    finally:
+        L.lib().zmi_set_option(L.OPT_GEMM_ROWS, old)
+
+
+def _batch_invariant_production_shape(L, name):
+    from zonos_vibes_amd.engine import rope_table
     N, K, ln, epi, mode = PROD_SHAPES[name]
     big = 128
     W = rnd(N, K, scale=0.03, seed=30)

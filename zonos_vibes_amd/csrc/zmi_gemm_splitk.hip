@@ -33,20 +33,26 @@ struct Shape {
 };
 constexpr int NWV = 8, NT = NWV * 64;  // wave g = column group cb * 8 + g
 constexpr int RT = 16;                 // rows per tile (one MFMA tile)
+// DN (dense pairs, zmi_gemv_impl.h gemm_rows_kernel): 4 waves, wave p = the column-group pair cb * 8 + 2p, +1 with a
+// 16-column B operand per k-half gathered from the two groups' M8 chunks: half the MFMAs and A-fragment reads of
+// the 8-wave form, the same bits
+constexpr int DNWV = 4, DNT = DNWV * 64;
 
 // Grid: (row group, K segment, column block), column blocks fastest. A row group is `rpg` consecutive 16-row tiles
 // (several row groups re-read the segment's weights, from L2 when they run together; speed only: a row's sums
 // do not depend on the grouping).
-template <int K>
-__global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb, int rpg) {
+template <int K, bool DN>
+__global__ __launch_bounds__(DN ? DNT : NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb, int rpg) {
   using S = Shape<K>;
   constexpr int NSEG = S::NSEG, KS = S::KS, NL = S::NL, KC = S::KC, SROW = S::SROW, TILE_BYTES = S::TILE_BYTES;
+  constexpr int NW = DN ? DNWV : NWV;  // waves
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x % (n_cb * NSEG), rg = blockIdx.x / (n_cb * NSEG);
   const int seg = b / n_cb, cb = b - seg * n_cb;  // consecutive blocks: one segment, neighbouring columns
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int g = cb * NWV + wave;
+  // the wave's group (DN: the group of lane l's column, 2 wave + ((l >> 3) & 1), of the wave's pair)
+  const int g = DN ? cb * NWV + 2 * wave + ((lane >> 3) & 1) : cb * NWV + wave;
   const int M = a.M, N = a.N;
   const int rt0 = rg * rpg, n_rt = min((M + RT - 1) / RT, rt0 + rpg);
   if (rt0 >= n_rt) return;
@@ -56,20 +62,33 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
   auto stage = [&](int rt, int buf) {  // the tile's rows of this segment, 1 KiB pieces spread over the waves
     const int row0 = rt * RT, rows = min(RT, M - row0);
     bf16_t* dst = tiles + (size_t)buf * (TILE_BYTES / 2);
-    for (int pc = wave; pc < rows * (KS / 512); pc += NWV) {
+    for (int pc = wave; pc < rows * (KS / 512); pc += NW) {
       const int r = pc / (KS / 512), p = pc - r * (KS / 512);
       dma_piece(X + (size_t)(row0 + r) * a.ldx + p * 512 + lane * 8, dst + r * SROW + p * 512);
     }
   };
   stage(rt0, 0);
-  // the wave's weights for this segment: group g, chunks seg * 16 .. + 15 (layout M8), all in flight
-  const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)g * KC + seg * NL) * 1024;
-  const __amdgpu_buffer_rsrc_t wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wbase), (short)0, NL * 1024, 0x00020000);
-  u32x4_t wf[NL];
+  // the wave's weights for this segment: group g, chunks seg * NL .. + NL - 1 (layout M8), all in flight
+  // (DN: k-half h of lane l's column = M8 lane (l & 7) + 8 h + 16 (l >> 4) of group g's chunk)
+  constexpr int NH = DN ? 2 : 1;
+  u32x4_t wf[NH][NL];
+  if constexpr (DN) {
+    const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)cb * NWV * KC + seg * NL) * 1024;
+    const __amdgpu_buffer_rsrc_t wrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wbase), (short)0, NWV * KC * 1024, 0x00020000);
+    const int vo = (g - cb * NWV) * KC * 1024 + ((lane & 7) + 16 * (lane >> 4)) * 16;
 #pragma unroll
-  for (int j = 0; j < NL; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, 2);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // the first tile's pieces (issued before)
+    for (int j = 0; j < NL; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wf[h][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, vo + 128 * h, j * 1024, 2);
+  } else {
+    const char* wbase = reinterpret_cast<const char*>(a.W) + ((size_t)g * KC + seg * NL) * 1024;
+    const __amdgpu_buffer_rsrc_t wrsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wbase), (short)0, NL * 1024, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) wf[0][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, 2);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NH * NL) : "memory");  // the first tile's pieces (issued before)
   for (int rt = rt0; rt < n_rt; ++rt) {
     __syncthreads();  // tile rt landed for every wave's pieces; buffer rt + 1 is free
     if (rt + 1 < n_rt) stage(rt + 1, (rt + 1 - rt0) & 1);
@@ -82,17 +101,17 @@ __global__ __launch_bounds__(NT) void splitk_kernel(const ZmiGemvArgs a, float* 
     for (int j = 0; j < NL; ++j) {
       const uint4 x0 = *reinterpret_cast<const uint4*>(xa + j * 64);
       const uint4 x1 = *reinterpret_cast<const uint4*>(xa + j * 64 + 32);
-      const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[j]);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), wv, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), wv, acc1, 0, 0, 0);
+      const bf16x8_t w0 = __builtin_bit_cast(bf16x8_t, wf[0][j]), w1 = __builtin_bit_cast(bf16x8_t, wf[NH - 1][j]);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), w0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), w1, acc1, 0, 0, 0);
     }
     // segment sum = k-half 0 (tile columns 0..7) + k-half 1 (columns 8..15 moved down): element q of lane l
-    // is row 4 (l >> 4) + q, column l & 15
+    // is row 4 (l >> 4) + q, column l & 15 (DN: both halves in place, column l & 15 of the pair)
     const int c = lane & 15, rb = (lane >> 4) * 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float v = acc0[q] + ror8(acc1[q]);
-      if (c < 8 && rb + q < rows) part[((size_t)seg * M + row0 + rb + q) * N + g * 8 + c] = v;
+      const float v = DN ? acc0[q] + acc1[q] : acc0[q] + ror8(acc1[q]);
+      if ((DN || c < 8) && rb + q < rows) part[((size_t)seg * M + row0 + rb + q) * N + g * 8 + (c & 7)] = v;
     }
     if (rt + 1 < n_rt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces
   }
@@ -179,11 +198,17 @@ int launch_splitk(const ZmiGemvArgs& a, int epi, float* part, const void* ln_w, 
   const int n_rg = std::max(1, std::min(n_rt, target / (n_cb * S::NSEG)));
   const int rpg = (n_rt + n_rg - 1) / n_rg;
   const size_t lds = 2 * (size_t)S::TILE_BYTES;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, false>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const hipError_t attr_dn = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, true>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   ZMI_CHECK(attr);
-  hipLaunchKernelGGL(splitk_kernel<K>, dim3(n_cb * S::NSEG * ((n_rt + rpg - 1) / rpg)), dim3(NT), lds, s, a, part,
-                     n_cb, rpg);
+  ZMI_CHECK(attr_dn);
+  const dim3 grid(n_cb * S::NSEG * ((n_rt + rpg - 1) / rpg));
+  if (zmi_option(ZMI_OPT_GEMM_ROWS) & 2)
+    hipLaunchKernelGGL((splitk_kernel<K, true>), grid, dim3(DNT), lds, s, a, part, n_cb, rpg);
+  else
+    hipLaunchKernelGGL((splitk_kernel<K, false>), grid, dim3(NT), lds, s, a, part, n_cb, rpg);
   ZMI_CHECK(hipGetLastError());
   if (ln_w) {
     hipLaunchKernelGGL(splitk_reduce_ln_kernel<S::NSEG>, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,

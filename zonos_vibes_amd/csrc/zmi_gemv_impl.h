@@ -714,11 +714,19 @@ __device__ __forceinline__ void dma_dword(const void* gsrc, void* ldp) {
                : "memory");
 }
 
-template <int EPI, int GPW>
-__global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const ZmiGemvArgs a, int n_cb, int n_rt,
-                                                                        int rpw) {
+//  * DN (dense pairs): each wave owns one PAIR of groups (16 columns) and feeds the MFMA a 16-column B operand per
+//    k-half: lane l = column l & 15 of the pair, k = 64 kc + 32 h + 8 (l >> 4) .. + 7, gathered from the two groups'
+//    M8 chunks at load time (lane (l & 7) + 8 h + 16 (l >> 4) of group 2p + ((l >> 3) & 1)). acc0 then holds every
+//    column's k-half-0 chain and acc1 its k-half-1 chain, the same products in the same MFMA accumulations as the M8
+//    form's columns 0..7 / 8..15 (a column's MFMA result does not depend on the column's place in the tile), and
+//    acc0 + acc1 is the M8 form's acc0 + ror8(acc1) for all 16 lanes: half the MFMAs of the M8 form, same bits.
+template <int EPI, int GPW, bool DN = false>
+__global__ __launch_bounds__(GR_G * 4 / GPW * 64 / (DN ? 2 : 1)) void gemm_rows_kernel(const ZmiGemvArgs a, int n_cb,
+                                                                                       int n_rt, int rpw) {
   constexpr int W = 4, NL = 8, RT = GR_RT, K = 2048, KC = K / 64, XROW = GR_XROW, NE = 2;
-  constexpr int NGS = GR_G / GPW, NWV = NGS * W;  // group sets, waves
+  // group sets (DN: pair sets, GPW pairs per wave), waves
+  constexpr int NGS = DN ? GR_G / 2 / GPW : GR_G / GPW, NWV = NGS * W;
+  static_assert(!DN || GPW == 1, "dense pairs: one pair per wave");
   // the activation tiles are DMA'd by the upper half of the waves only (PPW pieces each): the epilogue waves
   // (wave < 8) then never wait on memory inside the tile loop, so their output stores stay in flight
   constexpr int NDW = NWV / 2, PPW = RT * (K / 512) / NDW;
@@ -787,8 +795,20 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
   // the weight slices of the wave's groups (GPW NL x 16 B per lane), in flight at once, in chain order (chunk
   // j of every group before chunk j + 1): the first tile's chains follow them as they land. Re-read by the
   // other row groups of this column block from L2 (temporal).
-  u32x4_t wf[GPW][NL];
-  {
+  u32x4_t wf[DN ? 2 : GPW][NL];  // DN: wf[h][j] = k-half h of chunk j for the wave's pair
+  if constexpr (DN) {
+    // lane l: column l & 15 of pair gs (group cb * 8 + 2 gs + ((l >> 3) & 1), clamped: discarded), M8 lane
+    // (l & 7) + 8 h + 16 (l >> 4) of that group's chunk
+    const int grp = min(cb * GR_G + 2 * gs + ((lane >> 3) & 1), ngroups - 1) - cb * GR_G;
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(reinterpret_cast<const char*>(a.W) + (size_t)cb * GR_G * KC * 1024), (short)0,
+        GR_G * KC * 1024, 0x00020000);
+    const int vo = (grp * KC + wk * NL) * 1024 + ((lane & 7) + 16 * (lane >> 4)) * 16;
+#pragma unroll
+    for (int j = 0; j < NL; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wf[h][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, vo + 128 * h, j * 1024, 0);
+  } else {
     __amdgpu_buffer_rsrc_t wrsrc[GPW];
 #pragma unroll
     for (int h = 0; h < GPW; ++h)
@@ -821,11 +841,16 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
       for (int j = 0; j < NL; ++j) {
         const bf16x8_t x0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(xa + j * 64));
         const bf16x8_t x1 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(xa + j * 64 + 32));
+        if constexpr (DN) {
+          acc0[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, __builtin_bit_cast(bf16x8_t, wf[0][j]), acc0[0], 0, 0, 0);
+          acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, __builtin_bit_cast(bf16x8_t, wf[1][j]), acc1[0], 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int h = 0; h < GPW; ++h) {
-          const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[h][j]);
-          acc0[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, wv, acc0[h], 0, 0, 0);
-          acc1[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, wv, acc1[h], 0, 0, 0);
+          for (int h = 0; h < GPW; ++h) {
+            const bf16x8_t wv = __builtin_bit_cast(bf16x8_t, wf[h][j]);
+            acc0[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, wv, acc0[h], 0, 0, 0);
+            acc1[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, wv, acc1[h], 0, 0, 0);
+          }
         }
       }
     }
@@ -839,13 +864,19 @@ __global__ __launch_bounds__(GR_G * 4 / GPW * 64) void gemm_rows_kernel(const Zm
     }
     {
       const int c = lane & 15, rb = (lane >> 4) * 4;
+      if constexpr (DN) {
 #pragma unroll
-      for (int h = 0; h < GPW; ++h)
+        for (int q = 0; q < 4; ++q)
+          red[(((2 * gs + (c >> 3)) * W + wk) * 8 + (c & 7)) * RT + rb + q] = acc0[0][q] + acc1[0][q];
+      } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float v = acc0[h][q] + ror8(acc1[h][q]);
-          if (c < 8) red[(((gs + NGS * h) * W + wk) * 8 + c) * RT + rb + q] = v;
-        }
+        for (int h = 0; h < GPW; ++h)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc0[h][q] + ror8(acc1[h][q]);
+            if (c < 8) red[(((gs + NGS * h) * W + wk) * 8 + c) * RT + rb + q] = v;
+          }
+      }
     }
     // this tile's epilogue operands into registers before the buffer is re-filled
     uint32_t res_pre[NE] = {0u, 0u};
@@ -987,9 +1018,9 @@ hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
 // wide ones (heads 13.3 -> 11.6; qkv 7.6 -> 9.7, out_proj 5.8 -> 8.3)
 inline bool rows_form(int M, int N) { return M > 64 || (M > 32 && N >= 3072) || N >= 8192; }
 
-template <int EPI, int GPW>
+template <int EPI, int GPW, bool DN>
 hipError_t launch_rows(const ZmiGemvArgs& a, hipStream_t s) {
-  auto fn = gemm_rows_kernel<EPI, GPW>;
+  auto fn = gemm_rows_kernel<EPI, GPW, DN>;
   const int n_cb = (a.N / 8 + GR_G - 1) / GR_G;
   const int n_rt = (a.M + GR_RT - 1) / GR_RT;
   const int rpw = rows_per_wg(n_cb, n_rt, zmi_cu_count());  // one workgroup per CU
@@ -998,7 +1029,7 @@ hipError_t launch_rows(const ZmiGemvArgs& a, hipStream_t s) {
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
   if (attr != hipSuccess) return attr;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(GR_G * 4 / GPW * 64), GR_LDS, s, a, n_cb, n_rt, rpw);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(GR_G * 4 / GPW * 64 / (DN ? 2 : 1)), GR_LDS, s, a, n_cb, n_rt, rpw);
   return hipGetLastError();
 }
 
@@ -1009,7 +1040,7 @@ hipError_t launch(const ZmiGemvArgs& a, hipStream_t s) {
   const int g = groups_for(a, sh);
   if (a.K == 2048 && a.M > GR_RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO && a.groups == 0 &&
       zmi_option(ZMI_OPT_GEMM_ROWS) && rows_form(a.M, a.N))
-    return launch_rows<EPI, 2>(a, s);
+    return (zmi_option(ZMI_OPT_GEMM_ROWS) & 2) ? launch_rows<EPI, 1, true>(a, s) : launch_rows<EPI, 2, false>(a, s);
   if (g == 4 && sh.W == 4 && sh.NL == 8 && sh.RT == 16 && a.M > sh.RT && a.ln_w == nullptr && a.pro == ZMI_PRO_AUTO)
     return launch_p<4, 4, 8, 16, PRO_PLAIN, EPI, 0>(a, s);  // groups_for's many-row plain case only
 #define ZMI_SHAPE(G_, W_, NL_, RT_) \
