@@ -322,9 +322,11 @@ int zmi_mamba2_step(const ZmiMamba2Args* args, void* stream);
 /* Prefill from an empty state: M / seq_len sequences of seq_len rows (causal_conv1d_fn +
  * mamba_chunk_scan_combined of Mamba2.forward), leaving each sequence's final state and conv ring. */
 int zmi_mamba2_scan(const ZmiMamba2Args* args, int seq_len, void* stream);
-/* The same prefill, parallel form (the one HybridEngine runs): a conv + SiLU / dt launch into `ws`, then the
- * recurrence on 4 workgroups per (sequence, head), fused multiply-adds (fp32 rounding differs from
- * zmi_mamba2_scan's; both are checked against the oracle). ws: >= zmi_mamba2_scan_ws_bytes(M, d_ssm, nheads). */
+/* The same prefill, parallel forms (the one HybridEngine runs): a conv + SiLU / dt launch into `ws`, then either
+ * the state-space-dual matrix form (ZMI_OPT_SCAN_PQ 0, the default, sequences <= 256: y = (C B^T o decay) dt x on
+ * MFMA, one workgroup for y and one for the final state per (sequence, head)) or the recurrence on PQ workgroups per
+ * (sequence, head), fused multiply-adds (fp32 rounding differs from zmi_mamba2_scan's; all are checked against the
+ * oracle). ws: >= zmi_mamba2_scan_ws_bytes(M, d_ssm, nheads). */
 int zmi_mamba2_scan_ws(const ZmiMamba2Args* args, int seq_len, void* ws, int64_t ws_bytes, void* stream);
 int64_t zmi_mamba2_scan_ws_bytes(int m, int d_ssm, int nheads);
 /* layer_norm_fn(hidden, w, b, residual, prenorm=True): s = hidden + residual (fp32; hidden may be NULL:
@@ -393,8 +395,10 @@ int zmi_version(void);
  *          bit 3 512-row time tiles for the k7 convs where their grid is large enough (256 otherwise), bit 4 the
  *          256-row forms with 4 dedicated loader waves (768 threads).
  *   ZMI_OPT_DAC_STAGE_MIN (default 128): the staged form only where its grid has at least this many workgroups.
- *   ZMI_OPT_SCAN_PQ (default 4): zmi_mamba2_scan_ws workgroups per (sequence, head) (1, 2 or 4; each thread then
- *          owns 4 / PQ head dims x 8 state columns).
+ *   ZMI_OPT_SCAN_PQ (default 0): zmi_mamba2_scan_ws's form: 0 = the quadratic (SSD) form for sequences of up to
+ *          256 positions (MFMA tiles of C B^T, the decay matrix and the state sum; longer sequences take PQ 4), else
+ *          the recurrence on PQ workgroups per (sequence, head) (1, 2 or 4; each thread then owns 4 / PQ head dims x
+ *          8 state columns).
  *   ZMI_OPT_SPLITK_WGS (default 256): zmi_gemv_splitk splits the rows into groups of 16-row tiles until its grid
  *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,

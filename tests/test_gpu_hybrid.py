@@ -150,7 +150,7 @@ def test_mamba2_scan_matches_oracle(seq_len, form):
         nb = int(lib.zmi_mamba2_scan_ws_bytes(2 * seq_len, md["d_ssm"], md["nheads"]))
         ws = torch.full((nb,), 0xA5, dtype=torch.uint8, device=DEV)  # stale workspace must not matter
         old = lib.zmi_get_option(L.OPT_SCAN_PQ)
-        lib.zmi_set_option(L.OPT_SCAN_PQ, 0 if form == "scan_ssd" else 4)
+        lib.zmi_set_option(L.OPT_SCAN_PQ, 0 if form == "scan_ssd" else 4)  # the library default is the SSD form
         try:
             L.check(lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb, 0), form)
             assert lib.zmi_mamba2_scan_ws(ctypes.byref(a), seq_len, ws.data_ptr(), nb - 1, 0) != 0  # too small: refused

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--attn-variants", default="0,1,4,8", help="zmi_attention_variant choices to time")
     ap.add_argument("--spread", type=int, default=1, help="zmi_set_option(OPT_GEMV_SPREAD)")
-    ap.add_argument("--gemm-rows", default="1", help="zmi_set_option(OPT_GEMM_ROWS) values (0 off, 1 on) to time the GEMVs under")
+    ap.add_argument("--gemm-rows", default="3", help="zmi_set_option(OPT_GEMM_ROWS) values (0 off, 1 M8, 3 dense pairs) to time the GEMVs under")
     args = ap.parse_args()
     _lib.check(_lib.lib().zmi_set_option(_lib.OPT_GEMV_SPREAD, args.spread))
     dev = torch.device("cuda", 0)

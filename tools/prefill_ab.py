@@ -1,6 +1,6 @@
 """Prefill A/B, arms alternating in one process (weight placement moves timings between processes):
 
-    python tools/prefill_ab.py hybrid|transformer '[{"splitk_m_rows": 16}, {"splitk_m_rows": 0}]' [reps]
+    python tools/prefill_ab.py hybrid|transformer '[{"splitk_m_rows": 16}, {"splitk_m_rows": 0}]' [reps] [nocheck]
 
 An arm is a dict of engine attributes (set, then the plan rebuilt) plus optional "opt:<N>" library knobs
 (zmi_set_option). Each arm times the Lc + 1 = 161-row CFG prefill (322 rows) of the bench's C2 / C4 utterance
@@ -25,6 +25,7 @@ def main():
     kind = sys.argv[1]
     arms = json.loads(sys.argv[2])
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+    check = not (len(sys.argv) > 4 and sys.argv[4] == "nocheck")  # arms whose arithmetic differs: times only
     dev = torch.device("cuda", 0)
     from zonos_vibes_amd.config import zonos_v01_hybrid, zonos_v01_transformer
     cfg = zonos_v01_hybrid() if kind == "hybrid" else zonos_v01_transformer()
@@ -60,7 +61,8 @@ def main():
             e.release(0)
             if ref is None:
                 ref = lg
-            assert torch.equal(lg, ref), f"arm {arm}: prefill logits differ"
+            if check:
+                assert torch.equal(lg, ref), f"arm {arm}: prefill logits differ"
             if r:
                 times[i].append(st.elapsed_time(en))
     for arm, t in zip(arms, times):

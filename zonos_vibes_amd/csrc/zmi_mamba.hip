@@ -317,8 +317,8 @@ __global__ __launch_bounds__(256) void mamba2_scan2_kernel(const ZmiMamba2Args a
 // With cum[t] = sum_{tau <= t} A dt_tau (the log of the decays' product),
 //     y_t = sum_{s <= t} (C_t . B_s) exp(cum[t] - cum[s]) dt_s x_s + D x_t,
 //     state = sum_s exp(cum[T-1] - cum[s]) dt_s x_s B_s^T   (the recurrence's final state),
-// as MFMA tiles instead of T dependent steps. One 256-thread workgroup per (sequence, head, role): roles
-// 0 .. ceil(T / 32) - 1 write 32 rows of y, the last role the final state.
+// as MFMA tiles instead of T dependent steps. Two 1024-thread workgroups per (sequence, head): one writes y, 32 rows at
+// a time (the next block's C rows loaded under the current block's tiles), the other the final state.
 //   G = C_blk B^T          bf16 MFMA (B, C are the conv output, exactly bf16), fp32 sums;
 //   M = G exp(cum_t - cum_s) dt_s (s <= t, else 0), fp32, then split M = hi + lo into two bf16 terms;
 //   y = M_hi X + M_lo X    bf16 MFMA (x exactly bf16), fp32 sums, + D x, rounded to bf16;
@@ -326,25 +326,29 @@ __global__ __launch_bounds__(256) void mamba2_scan2_kernel(const ZmiMamba2Args a
 // cum is a fixed-shape scan (lane L owns positions 4L .. 4L + 3, lane totals by a shuffle scan) computed identically by
 // every role. Arithmetic differs from the recurrence in fp32 rounding (and the hi / lo split keeps ~16 mantissa bits
 // of M and W): checked against the oracle's recurrence like the scan forms.
-constexpr int SSD_TB = 32;      // y rows per workgroup
+constexpr int SSD_TB = 32;      // y rows per block of the y workgroup
+constexpr int SSD_NT = 1024;    // threads: 16 waves
 constexpr int SSD_TMAX = 256;   // longest sequence of this form
-constexpr int SSD_BROW = MB_DS + 8;  // B / C row stride (bf16)
+constexpr int SSD_BROW = MB_DS + 8;  // B / C row stride (bf16): 272 B, MFMA fragment reads spread over the banks
+constexpr int SSD_XROW = MB_HD + 8;  // x / W row stride (bf16)
 
+// Every operand stays row-major in LDS (position-major, as the workspace holds it: coalesced 16-byte copies, no
+// transposing stores); an MFMA operand whose k runs over positions is gathered as 8 bf16 of one column (8 ds_read_u16).
 struct SsdLds {
-  int S32, SP;  // positions rounded up to 32, transposed-row stride (bf16)
-  __device__ __host__ SsdLds(int T) : S32((T + 31) / 32 * 32), SP((T + 31) / 32 * 32 + 8) {}
-  // y role: cum, dt | B rows [T][SSD_BROW] | C rows [32][SSD_BROW] | M hi / lo [32][SP] | X^T [64][SP]
+  int S32;  // positions rounded up to 32
+  __device__ __host__ SsdLds(int T) : S32((T + 31) / 32 * 32) {}
+  // y role: cum, dt | B rows [S32][SSD_BROW] | C rows [32][SSD_BROW] | M hi / lo [32][S32 + 8] | x rows [S32][SSD_XROW]
+  __device__ __host__ int MP() const { return S32 + 8; }
   __device__ __host__ size_t b_off() const { return 2 * SSD_TMAX * 4; }
   __device__ __host__ size_t c_off() const { return b_off() + (size_t)S32 * SSD_BROW * 2; }
   __device__ __host__ size_t mh_off() const { return c_off() + (size_t)SSD_TB * SSD_BROW * 2; }
-  __device__ __host__ size_t ml_off() const { return mh_off() + (size_t)SSD_TB * SP * 2; }
-  __device__ __host__ size_t xt_off() const { return ml_off() + (size_t)SSD_TB * SP * 2; }
-  __device__ __host__ size_t y_bytes() const { return xt_off() + (size_t)MB_HD * SP * 2; }
-  // state role: cum, dt | B^T [128][SP] | W hi / lo [64][SP]
-  __device__ __host__ size_t bt_off() const { return 2 * SSD_TMAX * 4; }
-  __device__ __host__ size_t wh_off() const { return bt_off() + (size_t)MB_DS * SP * 2; }
-  __device__ __host__ size_t wl_off() const { return wh_off() + (size_t)MB_HD * SP * 2; }
-  __device__ __host__ size_t s_bytes() const { return wl_off() + (size_t)MB_HD * SP * 2; }
+  __device__ __host__ size_t ml_off() const { return mh_off() + (size_t)SSD_TB * MP() * 2; }
+  __device__ __host__ size_t x_off() const { return ml_off() + (size_t)SSD_TB * MP() * 2; }
+  __device__ __host__ size_t y_bytes() const { return x_off() + (size_t)S32 * SSD_XROW * 2; }
+  // state role: cum, dt | B rows [S32][SSD_BROW] | W hi / lo rows [S32][SSD_XROW]
+  __device__ __host__ size_t wh_off() const { return b_off() + (size_t)S32 * SSD_BROW * 2; }
+  __device__ __host__ size_t wl_off() const { return wh_off() + (size_t)S32 * SSD_XROW * 2; }
+  __device__ __host__ size_t s_bytes() const { return wl_off() + (size_t)S32 * SSD_XROW * 2; }
 };
 
 __device__ __forceinline__ f32x4_t mfma_bf16(const uint4& a, const uint4& b, f32x4_t c) {
@@ -352,24 +356,43 @@ __device__ __forceinline__ f32x4_t mfma_bf16(const uint4& a, const uint4& b, f32
                                                  0, 0);
 }
 
-__device__ __forceinline__ void split_bf16(float v, bf16_t& hi, bf16_t& lo) {
-  const uint32_t h = f2bf(v);
-  hi = (bf16_t)h;
-  lo = (bf16_t)f2bf(v - bf2f(h));
+// 8 bf16 of one column, rows r .. r + 7 of a row-major LDS array (stride in elements), packed as an MFMA k-fragment
+__device__ __forceinline__ uint4 gather8(const bf16_t* p, int stride) {
+  const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = (uint32_t)q[(2 * e) * stride] | ((uint32_t)q[(2 * e + 1) * stride] << 16);
+  return uint4{w[0], w[1], w[2], w[3]};
 }
 
-__global__ __launch_bounds__(256) void mamba2_ssd_kernel(const ZmiMamba2Args a, int seq_len, const bf16_t* xc,
+__device__ __forceinline__ uint32_t split_bf16(float v, uint32_t* lo) {
+  const uint32_t h = f2bf(v);
+  *lo = f2bf(v - bf2f(h));
+  return h;
+}
+
+__global__ __launch_bounds__(SSD_NT) void mamba2_ssd_kernel(const ZmiMamba2Args a, int seq_len, const bf16_t* xc,
                                                          const float* dts) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int T = seq_len, nroles = (T + SSD_TB - 1) / SSD_TB + 1;
-  const int role = blockIdx.x % nroles, sh = blockIdx.x / nroles, h = sh % a.nheads, sq = sh / a.nheads;
+  const int T = seq_len;
+  const int role = blockIdx.x & 1, sh = blockIdx.x >> 1, h = sh % a.nheads, sq = sh / a.nheads;
   const int row0 = sq * T, conv_dim = a.d_ssm + 2 * MB_DS;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const SsdLds L(T);
   float* cum = reinterpret_cast<float*>(smem);
   float* dtl = cum + SSD_TMAX;
   const float Ah = a.A[h];
-  // (1) dt and cum for every position (the same fixed-shape scan in every role)
+  const bool state_role = role == 1;
+  const int s32 = L.S32;
+  bf16_t* Bs = reinterpret_cast<bf16_t*>(smem + L.b_off());
+  // (1) B rows s < s_end (zero to s32) for both roles; dt and cum for every position (the same fixed-shape scan in
+  // every role: lane L owns positions 4L .. 4L + 3)
+  for (int i = t; i < s32 * (MB_DS / 8); i += SSD_NT) {
+    const int r = i / (MB_DS / 8), c = i % (MB_DS / 8);
+    uint4 v = uint4{0u, 0u, 0u, 0u};
+    if (r < T) v = *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + r) * conv_dim + a.d_ssm + 8 * c);
+    *reinterpret_cast<uint4*>(Bs + r * SSD_BROW + 8 * c) = v;
+  }
   if (wave == 0) {
     float v[4], run = 0.f;
 #pragma unroll
@@ -390,129 +413,143 @@ __global__ __launch_bounds__(256) void mamba2_ssd_kernel(const ZmiMamba2Args a, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) cum[4 * lane + i] = excl + v[i];
   }
-  const bool state_role = role == nroles - 1;
   if (!state_role) {
-    const int t0 = role * SSD_TB, tn = min(SSD_TB, T - t0), s_end = t0 + tn, s32 = (s_end + 31) / 32 * 32;
-    bf16_t* Bs = reinterpret_cast<bf16_t*>(smem + L.b_off());
     bf16_t* Cs = reinterpret_cast<bf16_t*>(smem + L.c_off());
     bf16_t* Mh = reinterpret_cast<bf16_t*>(smem + L.mh_off());
     bf16_t* Ml = reinterpret_cast<bf16_t*>(smem + L.ml_off());
-    bf16_t* Xt = reinterpret_cast<bf16_t*>(smem + L.xt_off());
-    // (2) B rows s < s_end (zero to s32), C rows of the block, X^T [p][s] (zero past s_end), M zeroed
-    for (int i = t; i < s32 * (MB_DS / 8); i += 256) {
-      const int r = i / (MB_DS / 8), c = i % (MB_DS / 8);
+    bf16_t* Xs = reinterpret_cast<bf16_t*>(smem + L.x_off());
+    const int MP = L.MP();
+    // (2) x rows (zero to s32); the first row block's C rows into registers (2 x 16 B per thread), each later block's
+    // loaded while the previous one computes
+    for (int i = t; i < s32 * (MB_HD / 8); i += SSD_NT) {
+      const int r = i / (MB_HD / 8), c = i % (MB_HD / 8);
       uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (r < s_end) v = *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + r) * conv_dim + a.d_ssm + 8 * c);
-      *reinterpret_cast<uint4*>(Bs + r * SSD_BROW + 8 * c) = v;
+      if (r < T) v = *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + r) * conv_dim + h * MB_HD + 8 * c);
+      *reinterpret_cast<uint4*>(Xs + r * SSD_XROW + 8 * c) = v;
     }
-    for (int i = t; i < SSD_TB * (MB_DS / 8); i += 256) {
-      const int r = i / (MB_DS / 8), c = i % (MB_DS / 8);
-      uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (r < tn) v = *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + t0 + r) * conv_dim + a.d_ssm + MB_DS + 8 * c);
-      *reinterpret_cast<uint4*>(Cs + r * SSD_BROW + 8 * c) = v;
-    }
-    for (int i = t; i < s32 * (MB_HD / 2); i += 256) {  // x pairs, transposed
-      const int r = i / (MB_HD / 2), c = i % (MB_HD / 2);
-      uint32_t v = 0u;
-      if (r < s_end) v = *reinterpret_cast<const uint32_t*>(xc + (size_t)(row0 + r) * conv_dim + h * MB_HD + 2 * c);
-      Xt[(2 * c) * L.SP + r] = (bf16_t)(v & 0xffffu);
-      Xt[(2 * c + 1) * L.SP + r] = (bf16_t)(v >> 16);
-    }
-    for (int i = t; i < SSD_TB * L.SP / 2; i += 256) {
-      reinterpret_cast<uint32_t*>(Mh)[i] = 0u;
-      reinterpret_cast<uint32_t*>(Ml)[i] = 0u;
-    }
-    __syncthreads();
-    // (3) G and M tiles (16 t x 16 s), s <= t only: wave w takes tiles w, w + 4, ...
-    const int ntile_s = (s_end + 15) / 16;
-    for (int tile = wave; tile < 2 * ntile_s; tile += 4) {
-      const int ti = tile & 1, si = tile >> 1;
-      if (16 * ti >= tn || 16 * si > t0 + 16 * ti + 15) continue;
-      f32x4_t g = {0.f, 0.f, 0.f, 0.f};
+    constexpr int CP = SSD_TB * (MB_DS / 8), CPT = (CP + SSD_NT - 1) / SSD_NT;  // C pieces (16 B), per thread
+    uint4 cr[CPT];
+    auto load_c = [&](int tb0) {
 #pragma unroll
-      for (int kk = 0; kk < MB_DS / 32; ++kk) {
-        const uint4 av = *reinterpret_cast<const uint4*>(Cs + (16 * ti + (lane & 15)) * SSD_BROW + 32 * kk + 8 * (lane >> 4));
-        const uint4 bv = *reinterpret_cast<const uint4*>(Bs + (16 * si + (lane & 15)) * SSD_BROW + 32 * kk + 8 * (lane >> 4));
-        g = mfma_bf16(av, bv, g);
+      for (int j = 0; j < CPT; ++j) {
+        const int i = t + SSD_NT * j, r = i / (MB_DS / 8), c = i % (MB_DS / 8);
+        cr[j] = i < CP && tb0 + r < T
+                    ? *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + tb0 + r) * conv_dim + a.d_ssm + MB_DS + 8 * c)
+                    : uint4{0u, 0u, 0u, 0u};
       }
-      const int s = 16 * si + (lane & 15);
+    };
+    load_c(0);
+    const float Dh = a.D[h];
+    for (int t0 = 0; t0 < T; t0 += SSD_TB) {
+      const int tn = min(SSD_TB, T - t0), s_end = t0 + tn, sk = (s_end + 31) / 32;  // k-blocks of 32 positions
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int tl = 16 * ti + 4 * (lane >> 4) + i, tt = t0 + tl;
-        float m = 0.f;
-        if (tl < tn && s <= tt) m = g[i] * expf(cum[tt] - cum[s]) * dtl[s];
-        split_bf16(m, Mh[tl * L.SP + s], Ml[tl * L.SP + s]);
+      for (int j = 0; j < CPT; ++j) {
+        const int i = t + SSD_NT * j, r = i / (MB_DS / 8), c = i % (MB_DS / 8);
+        if (i < CP) *reinterpret_cast<uint4*>(Cs + r * SSD_BROW + 8 * c) = cr[j];
       }
-    }
-    __syncthreads();
-    // (4) y tiles (16 t x 16 p): wave w -> t tile w & 1, p tiles 2 (w >> 1), + 1
-    const int ti = wave & 1;
-    if (16 * ti < tn) {
+      __syncthreads();  // C block (and, the first time, B / x / cum) visible; the previous block's y reads are done
+      if (t0 + SSD_TB < T) load_c(t0 + SSD_TB);
+      // (3) M tiles (16 t x 16 s) over s < 32 sk: G = C B^T on the tiles that reach s <= t, zeros elsewhere
+      for (int tile = wave; tile < 4 * sk; tile += SSD_NT / 64) {
+        const int ti = tile & 1, si = tile >> 1;
+        const bool live = 16 * ti < tn && 16 * si <= t0 + 16 * ti + 15;
+        f32x4_t g = {0.f, 0.f, 0.f, 0.f};
+        if (live) {
 #pragma unroll
-      for (int pj2 = 0; pj2 < 2; ++pj2) {
-        const int pj = 2 * (wave >> 1) + pj2;
-        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-        for (int kk = 0; kk < s32 / 32; ++kk) {
-          const int mo = (16 * ti + (lane & 15)) * L.SP + 32 * kk + 8 * (lane >> 4);
-          const uint4 bv = *reinterpret_cast<const uint4*>(Xt + (16 * pj + (lane & 15)) * L.SP + 32 * kk + 8 * (lane >> 4));
-          acc = mfma_bf16(*reinterpret_cast<const uint4*>(Mh + mo), bv, acc);
-          acc = mfma_bf16(*reinterpret_cast<const uint4*>(Ml + mo), bv, acc);
+          for (int kk = 0; kk < MB_DS / 32; ++kk) {
+            const uint4 av = *reinterpret_cast<const uint4*>(Cs + (16 * ti + (lane & 15)) * SSD_BROW + 32 * kk + 8 * (lane >> 4));
+            const uint4 bv = *reinterpret_cast<const uint4*>(Bs + (16 * si + (lane & 15)) * SSD_BROW + 32 * kk + 8 * (lane >> 4));
+            g = mfma_bf16(av, bv, g);
+          }
         }
-        const int p = 16 * pj + (lane & 15);
-        const float Dh = a.D[h];
+        const int s = 16 * si + (lane & 15);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int tl = 16 * ti + 4 * (lane >> 4) + i;
-          if (tl < tn) {
-            const float x = bf2f((uint32_t)(uint16_t)Xt[p * L.SP + t0 + tl]);
-            reinterpret_cast<bf16_t*>(a.y)[(size_t)(row0 + t0 + tl) * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(acc[i] + x * Dh);
+          const int tl = 16 * ti + 4 * (lane >> 4) + i, tt = t0 + tl;
+          float m = 0.f;
+          if (live && tl < tn && s <= tt) m = g[i] * expf(cum[tt] - cum[s]) * dtl[s];
+          uint32_t lo;
+          const uint32_t hi = split_bf16(m, &lo);
+          Mh[tl * MP + s] = (bf16_t)hi;
+          Ml[tl * MP + s] = (bf16_t)lo;
+        }
+      }
+      __syncthreads();
+      // (4) y tiles (16 t x 16 p): wave w < 8 -> t tile w & 1, p tile w >> 1; the x fragment of a k-block (8 consecutive
+      // positions of column p) gathered from the row-major x rows
+      const int ti = wave & 1;
+      if (wave < 8 && 16 * ti < tn) {
+        {
+          const int pj = wave >> 1, p = 16 * pj + (lane & 15);
+          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+          for (int kk = 0; kk < sk; ++kk) {
+            const int mo = (16 * ti + (lane & 15)) * MP + 32 * kk + 8 * (lane >> 4);
+            const uint4 bv = gather8(Xs + (32 * kk + 8 * (lane >> 4)) * SSD_XROW + p, SSD_XROW);
+            acc = mfma_bf16(*reinterpret_cast<const uint4*>(Mh + mo), bv, acc);
+            acc = mfma_bf16(*reinterpret_cast<const uint4*>(Ml + mo), bv, acc);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int tl = 16 * ti + 4 * (lane >> 4) + i;
+            if (tl < tn) {
+              const float x = bf2f((uint32_t)reinterpret_cast<const uint16_t*>(Xs)[(t0 + tl) * SSD_XROW + p]);
+              reinterpret_cast<bf16_t*>(a.y)[(size_t)(row0 + t0 + tl) * a.ldy + h * MB_HD + p] =
+                  (bf16_t)f2bf(acc[i] + x * Dh);
+            }
           }
         }
       }
     }
   } else {
-    const int s32 = L.S32;
-    bf16_t* Bt = reinterpret_cast<bf16_t*>(smem + L.bt_off());
     bf16_t* Wh = reinterpret_cast<bf16_t*>(smem + L.wh_off());
     bf16_t* Wl = reinterpret_cast<bf16_t*>(smem + L.wl_off());
     __syncthreads();  // cum / dt
     const float cT = cum[T - 1];
-    // (2) B^T [n][s] and W^T [p][s] = exp(cum[T-1] - cum[s]) dt_s x_s[p] (hi / lo), zero past T
-    for (int i = t; i < s32 * (MB_DS / 2); i += 256) {
-      const int r = i / (MB_DS / 2), c = i % (MB_DS / 2);
-      uint32_t v = 0u;
-      if (r < T) v = *reinterpret_cast<const uint32_t*>(xc + (size_t)(row0 + r) * conv_dim + a.d_ssm + 2 * c);
-      Bt[(2 * c) * L.SP + r] = (bf16_t)(v & 0xffffu);
-      Bt[(2 * c + 1) * L.SP + r] = (bf16_t)(v >> 16);
-    }
-    for (int i = t; i < s32 * (MB_HD / 2); i += 256) {
-      const int r = i / (MB_HD / 2), c = i % (MB_HD / 2);
-      float w0 = 0.f, w1 = 0.f;
+    // (2) W rows [s][p] = exp(cum[T-1] - cum[s]) dt_s x_s[p] as hi / lo bf16, zero past T
+    for (int i = t; i < s32 * (MB_HD / 8); i += SSD_NT) {
+      const int r = i / (MB_HD / 8), c = i % (MB_HD / 8);
+      uint32_t hv[4] = {0u, 0u, 0u, 0u}, lv[4] = {0u, 0u, 0u, 0u};
       if (r < T) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(xc + (size_t)(row0 + r) * conv_dim + h * MB_HD + 2 * c);
+        const uint4 v = *reinterpret_cast<const uint4*>(xc + (size_t)(row0 + r) * conv_dim + h * MB_HD + 8 * c);
         const float w = expf(cT - cum[r]) * dtl[r];
-        w0 = w * bf2f(v);
-        w1 = w * bf2f(v >> 16);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t l0, l1;
+          const uint32_t h0 = split_bf16(w * bf2f(u[e]), &l0), h1 = split_bf16(w * bf2f(u[e] >> 16), &l1);
+          hv[e] = h0 | (h1 << 16);
+          lv[e] = l0 | (l1 << 16);
+        }
       }
-      split_bf16(w0, Wh[(2 * c) * L.SP + r], Wl[(2 * c) * L.SP + r]);
-      split_bf16(w1, Wh[(2 * c + 1) * L.SP + r], Wl[(2 * c + 1) * L.SP + r]);
+      *reinterpret_cast<uint4*>(Wh + r * SSD_XROW + 8 * c) = uint4{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<uint4*>(Wl + r * SSD_XROW + 8 * c) = uint4{lv[0], lv[1], lv[2], lv[3]};
     }
     __syncthreads();
-    // (3) state tiles (16 p x 16 n): 4 x 8 tiles, wave w -> p tile w, n tiles 0..7
+    // (3) state tiles (16 p x 16 n): wave w -> p tile w & 3, n tiles 4 (w >> 2) .. + 3; A = W^T and B fragments
+    // gathered per k-block
+    constexpr int NPW = MB_DS / 16 / (SSD_NT / 64 / 4);  // n tiles per wave
     const int kv = a.row_kv ? a.row_kv[row0] : sq;
     bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + ((size_t)kv * a.nheads + h) * MB_HD * MB_DS;
-    const int pi = wave;
-    for (int ni = 0; ni < MB_DS / 16; ++ni) {
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      for (int kk = 0; kk < s32 / 32; ++kk) {
-        const int wo = (16 * pi + (lane & 15)) * L.SP + 32 * kk + 8 * (lane >> 4);
-        const uint4 bv = *reinterpret_cast<const uint4*>(Bt + (16 * ni + (lane & 15)) * L.SP + 32 * kk + 8 * (lane >> 4));
-        acc = mfma_bf16(*reinterpret_cast<const uint4*>(Wh + wo), bv, acc);
-        acc = mfma_bf16(*reinterpret_cast<const uint4*>(Wl + wo), bv, acc);
-      }
-      const int n = 16 * ni + (lane & 15);
+    const int pi = wave & 3, nb = (wave >> 2) * NPW;
+    f32x4_t acc[NPW];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st[(size_t)(16 * pi + 4 * (lane >> 4) + i) * MB_DS + n] = (bf16_t)f2bf(acc[i]);
+    for (int ni = 0; ni < NPW; ++ni) acc[ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < s32 / 32; ++kk) {
+      const int r = 32 * kk + 8 * (lane >> 4);
+      const uint4 ah = gather8(Wh + r * SSD_XROW + 16 * pi + (lane & 15), SSD_XROW);
+      const uint4 al = gather8(Wl + r * SSD_XROW + 16 * pi + (lane & 15), SSD_XROW);
+#pragma unroll
+      for (int ni = 0; ni < NPW; ++ni) {
+        const uint4 bv = gather8(Bs + r * SSD_BROW + 16 * (nb + ni) + (lane & 15), SSD_BROW);
+        acc[ni] = mfma_bf16(ah, bv, acc[ni]);
+        acc[ni] = mfma_bf16(al, bv, acc[ni]);
+      }
+    }
+#pragma unroll
+    for (int ni = 0; ni < NPW; ++ni) {
+      const int n = 16 * (nb + ni) + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[(size_t)(16 * pi + 4 * (lane >> 4) + i) * MB_DS + n] = (bf16_t)f2bf(acc[ni][i]);
     }
   }
 }
@@ -705,8 +742,7 @@ extern "C" int zmi_mamba2_scan_ws(const ZmiMamba2Args* a, int seq_len, void* ws,
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mamba2_ssd_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     ZMI_CHECK(attr);
-    const int nroles = (seq_len + SSD_TB - 1) / SSD_TB + 1;
-    hipLaunchKernelGGL(mamba2_ssd_kernel, dim3((unsigned)(a->M / seq_len * a->nheads * nroles)), dim3(256), lds, s, *a,
+    hipLaunchKernelGGL(mamba2_ssd_kernel, dim3((unsigned)(a->M / seq_len * a->nheads * 2)), dim3(SSD_NT), lds, s, *a,
                        seq_len, (const bf16_t*)xc, (const float*)dts);
     ZMI_CHECK(hipGetLastError());
     return 0;
