@@ -179,6 +179,10 @@ class HipEngine:
         # decode steps whose slots all sample greedily use the one-workgroup-per-slot sampler
         # (zmi_sample_step_greedy: identical results, no in-launch hand-off between codebooks)
         self.greedy_sampler = True
+        # decode steps per hipGraph replay (a run of k steps replays the graph of graph_steps steps k // graph_steps
+        # times, then the one-step graph for the rest; the same launches in the same order). C2 step at position
+        # 591: 950.2-950.5 us with 1, 946.8 with 4, 945.8-946.0 with 8, 945.2 with 16 (profiles/r05_graph_steps_ab.jsonl)
+        self.graph_steps = 16
         # generate_batch steps only slots 0 .. the highest busy one (bucketed), not every slot
         self.batch_shrink = True
         self.slot_greedy = [False] * self.S
@@ -707,13 +711,16 @@ class HipEngine:
                 item()
         self._sample(self.logits, noise, 0, 0, rows // 2)
 
-    def capture(self, slots: int | None = None, form: str = "none"):
+    def capture(self, slots: int | None = None, form: str = "none", steps: int = 1):
+        """The hipGraph of `steps` consecutive decode steps of slots 0 .. slots-1 in one attention form (the loop
+        state lives on the device, so a graph of several steps is the one-step graph's launches repeated)."""
         rows = self._rows(slots)
-        key = (rows, form, self._greedy_step(0, rows // 2))
+        key = (rows, form, self._greedy_step(0, rows // 2), steps)
         if key not in self._graphs:
             _lib.check(self.lib.zmi_graph_begin(self.sptr), "graph_begin")
             try:
-                self.enqueue_step(slots=rows // 2, form=form)
+                for _ in range(steps):
+                    self.enqueue_step(slots=rows // 2, form=form)
             finally:
                 g = ctypes.c_void_p()
                 _lib.check(self.lib.zmi_graph_end(self.sptr, ctypes.byref(g)), "graph_end")
@@ -732,7 +739,12 @@ class HipEngine:
         s = self._rows(slots) // 2
         for k, form in self._segments(n, s):
             if use_graph:
-                _lib.check(self.lib.zmi_graph_launch(self.capture(s, form), k, self.sptr), "graph_launch")
+                u = self.graph_steps
+                if u > 1 and k >= u:  # runs of u-step graphs, then the remainder one step per replay
+                    _lib.check(self.lib.zmi_graph_launch(self.capture(s, form, u), k // u, self.sptr), "graph_launch")
+                if k % u or u <= 1:
+                    _lib.check(self.lib.zmi_graph_launch(self.capture(s, form), k % u if u > 1 else k, self.sptr),
+                               "graph_launch")
             else:
                 for _ in range(k):
                     self.enqueue_step(slots=s, form=form)
