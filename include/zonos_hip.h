@@ -400,11 +400,14 @@ int zmi_version(void);
  *          the recurrence on PQ workgroups per (sequence, head) (1, 2 or 4; each thread then owns 4 / PQ head dims x
  *          8 state columns).
  *   ZMI_OPT_SPLITK_WGS (default 256): zmi_gemv_splitk splits the rows into groups of 16-row tiles until its grid
- *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group. */
+ *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group.
+ *   ZMI_OPT_SPLITK_STAGE (default 1): zmi_gemv_splitk stages 2 (K segment 1024) or 4 (512) 16-row tiles per LDS
+ *          buffer, so twice the activation bytes are in flight per CU (~132 KB of LDS); 0 = one tile per buffer. */
 enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
        ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
        ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
-       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_SPLITK_WGS = 16, ZMI_OPT_COUNT = 17 };
+       ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_SPLITK_WGS = 16, ZMI_OPT_SPLITK_STAGE = 17,
+       ZMI_OPT_COUNT = 18 };
 int zmi_set_option(int which, int value);
 int zmi_get_option(int which);
 

@@ -15,11 +15,12 @@ pytestmark = pytest.mark.gpu
 D, F = 2048, 8192
 
 
+@pytest.mark.parametrize("stage", [1, 0])  # ZMI_OPT_SPLITK_STAGE: several 16-row tiles per LDS stage buffer
 @pytest.mark.parametrize("rows_opt", [1, 3])  # ZMI_OPT_GEMM_ROWS bit 1: the dense-pair MFMA form
 @pytest.mark.parametrize("wgs", [256, 0, 1024])
 @pytest.mark.parametrize("K", [F, 4096, D])
 @pytest.mark.parametrize("M", [1, 16, 17, 64, 65, 128, 322])
-def test_splitk_bit_identical_to_gemv(M, K, wgs, rows_opt):
+def test_splitk_bit_identical_to_gemv(M, K, wgs, rows_opt, stage):
     L = _lib()
     epi = L.EPI_STORE if K == 4096 else L.EPI_RESIDUAL
     W = rnd(D, K, scale=0.03, seed=70)
@@ -40,15 +41,16 @@ def test_splitk_bit_identical_to_gemv(M, K, wgs, rows_opt):
     nf = L.lib().zmi_gemv_splitk_floats(M, D)
     part = torch.full((nf,), float("nan"), dtype=torch.float32, device=DEV)
     a = args(got)
-    old = L.lib().zmi_get_option(L.OPT_SPLITK_WGS), L.lib().zmi_get_option(L.OPT_GEMM_ROWS)
-    L.lib().zmi_set_option(L.OPT_SPLITK_WGS, wgs)
-    L.lib().zmi_set_option(L.OPT_GEMM_ROWS, rows_opt)
+    knobs = {L.OPT_SPLITK_WGS: wgs, L.OPT_GEMM_ROWS: rows_opt, L.OPT_SPLITK_STAGE: stage}
+    old = {k: L.lib().zmi_get_option(k) for k in knobs}
+    for k, v in knobs.items():
+        L.lib().zmi_set_option(k, v)
     try:
         L.check(L.lib().zmi_gemv_splitk(ctypes.byref(a), epi, part.data_ptr(), nf, stream_ptr()), "splitk")
         torch.cuda.synchronize()
     finally:
-        L.lib().zmi_set_option(L.OPT_SPLITK_WGS, old[0])
-        L.lib().zmi_set_option(L.OPT_GEMM_ROWS, old[1])
+        for k, v in old.items():
+            L.lib().zmi_set_option(k, v)
     assert torch.equal(got, ref), (got != ref).nonzero()[:4].tolist()
 
 

@@ -34,6 +34,7 @@ OPT_DAC_STAGE = 13
 OPT_DAC_STAGE_MIN = 14
 OPT_SCAN_PQ = 15
 OPT_SPLITK_WGS = 16
+OPT_SPLITK_STAGE = 17
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
 PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3

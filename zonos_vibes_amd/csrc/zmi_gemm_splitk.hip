@@ -30,6 +30,7 @@ struct Shape {
   static constexpr int NSEG = K == 8192 ? 8 : 4, KS = K / NSEG, NL = KS / 64, KC = K / 64;
   static constexpr int SROW = KS + 8;  // LDS row stride (bf16): bank-spread A reads
   static constexpr int TILE_BYTES = 16 * SROW * 2;
+  static constexpr int RTS = KS >= 1024 ? 2 : 4;  // 16-row tiles per stage: two stages fill ~132 KB of LDS
 };
 constexpr int NWV = 8, NT = NWV * 64;  // wave g = column group cb * 8 + g
 constexpr int RT = 16;                 // rows per tile (one MFMA tile)
@@ -41,7 +42,7 @@ constexpr int DNWV = 4, DNT = DNWV * 64;
 // Grid: (row group, K segment, column block), column blocks fastest. A row group is `rpg` consecutive 16-row tiles
 // (several row groups re-read the segment's weights, from L2 when they run together; speed only: a row's sums
 // do not depend on the grouping).
-template <int K, bool DN>
+template <int K, bool DN, int RTS>
 __global__ __launch_bounds__(DN ? DNT : NT) void splitk_kernel(const ZmiGemvArgs a, float* part, int n_cb, int rpg) {
   using S = Shape<K>;
   constexpr int NSEG = S::NSEG, KS = S::KS, NL = S::NL, KC = S::KC, SROW = S::SROW, TILE_BYTES = S::TILE_BYTES;
@@ -56,18 +57,20 @@ __global__ __launch_bounds__(DN ? DNT : NT) void splitk_kernel(const ZmiGemvArgs
   const int M = a.M, N = a.N;
   const int rt0 = rg * rpg, n_rt = min((M + RT - 1) / RT, rt0 + rpg);
   if (rt0 >= n_rt) return;
-  bf16_t* tiles = reinterpret_cast<bf16_t*>(smem);  // two tile buffers
+  // a stage = RTS 16-row tiles (two stage buffers): the next stage's rows are in flight while this one's tiles run
+  const int n_st = (n_rt - rt0 + RTS - 1) / RTS;
+  bf16_t* tiles = reinterpret_cast<bf16_t*>(smem);
   const bf16_t* X = reinterpret_cast<const bf16_t*>(a.X) + (size_t)seg * KS;
 
-  auto stage = [&](int rt, int buf) {  // the tile's rows of this segment, 1 KiB pieces spread over the waves
-    const int row0 = rt * RT, rows = min(RT, M - row0);
-    bf16_t* dst = tiles + (size_t)buf * (TILE_BYTES / 2);
+  auto stage = [&](int st, int buf) {  // the stage's rows of this segment, 1 KiB pieces spread over the waves
+    const int row0 = (rt0 + st * RTS) * RT, rows = min(min(RTS * RT, M - row0), (n_rt - rt0 - st * RTS) * RT);
+    bf16_t* dst = tiles + (size_t)buf * RTS * (TILE_BYTES / 2);
     for (int pc = wave; pc < rows * (KS / 512); pc += NW) {
       const int r = pc / (KS / 512), p = pc - r * (KS / 512);
       dma_piece(X + (size_t)(row0 + r) * a.ldx + p * 512 + lane * 8, dst + r * SROW + p * 512);
     }
   };
-  stage(rt0, 0);
+  stage(0, 0);
   // the wave's weights for this segment: group g, chunks seg * NL .. + NL - 1 (layout M8), all in flight
   // (DN: k-half h of lane l's column = M8 lane (l & 7) + 8 h + 16 (l >> 4) of group g's chunk)
   constexpr int NH = DN ? 2 : 1;
@@ -88,32 +91,37 @@ __global__ __launch_bounds__(DN ? DNT : NT) void splitk_kernel(const ZmiGemvArgs
 #pragma unroll
     for (int j = 0; j < NL; ++j) wf[0][j] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane * 16, j * 1024, 2);
   }
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NH * NL) : "memory");  // the first tile's pieces (issued before)
-  for (int rt = rt0; rt < n_rt; ++rt) {
-    __syncthreads();  // tile rt landed for every wave's pieces; buffer rt + 1 is free
-    if (rt + 1 < n_rt) stage(rt + 1, (rt + 1 - rt0) & 1);
-    const int row0 = rt * RT, rows = min(RT, M - row0);
-    const bf16_t* xs = tiles + (size_t)((rt - rt0) & 1) * (TILE_BYTES / 2);
-    f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const int ar = min(lane & 15, rows - 1);
-    const bf16_t* xa = xs + ar * SROW + (lane >> 4) * 8;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NH * NL) : "memory");  // the first stage's pieces (issued before)
+  for (int st = 0; st < n_st; ++st) {
+    __syncthreads();  // stage st landed for every wave's pieces; the other buffer is free
+    if (st + 1 < n_st) stage(st + 1, (st + 1) & 1);
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const uint4 x0 = *reinterpret_cast<const uint4*>(xa + j * 64);
-      const uint4 x1 = *reinterpret_cast<const uint4*>(xa + j * 64 + 32);
-      const bf16x8_t w0 = __builtin_bit_cast(bf16x8_t, wf[0][j]), w1 = __builtin_bit_cast(bf16x8_t, wf[NH - 1][j]);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), w0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), w1, acc1, 0, 0, 0);
-    }
-    // segment sum = k-half 0 (tile columns 0..7) + k-half 1 (columns 8..15 moved down): element q of lane l
-    // is row 4 (l >> 4) + q, column l & 15 (DN: both halves in place, column l & 15 of the pair)
-    const int c = lane & 15, rb = (lane >> 4) * 4;
+    for (int u = 0; u < RTS; ++u) {
+      const int rt = rt0 + st * RTS + u;
+      if (rt >= n_rt) break;
+      const int row0 = rt * RT, rows = min(RT, M - row0);
+      const bf16_t* xs = tiles + ((size_t)(st & 1) * RTS + u) * (TILE_BYTES / 2);
+      f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const int ar = min(lane & 15, rows - 1);
+      const bf16_t* xa = xs + ar * SROW + (lane >> 4) * 8;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float v = DN ? acc0[q] + acc1[q] : acc0[q] + ror8(acc1[q]);
-      if ((DN || c < 8) && rb + q < rows) part[((size_t)seg * M + row0 + rb + q) * N + g * 8 + (c & 7)] = v;
+      for (int j = 0; j < NL; ++j) {
+        const uint4 x0 = *reinterpret_cast<const uint4*>(xa + j * 64);
+        const uint4 x1 = *reinterpret_cast<const uint4*>(xa + j * 64 + 32);
+        const bf16x8_t w0 = __builtin_bit_cast(bf16x8_t, wf[0][j]), w1 = __builtin_bit_cast(bf16x8_t, wf[NH - 1][j]);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x0), w0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, x1), w1, acc1, 0, 0, 0);
+      }
+      // segment sum = k-half 0 (tile columns 0..7) + k-half 1 (columns 8..15 moved down): element q of lane l
+      // is row 4 (l >> 4) + q, column l & 15 (DN: both halves in place, column l & 15 of the pair)
+      const int c = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = DN ? acc0[q] + acc1[q] : acc0[q] + ror8(acc1[q]);
+        if ((DN || c < 8) && rb + q < rows) part[((size_t)seg * M + row0 + rb + q) * N + g * 8 + (c & 7)] = v;
+      }
     }
-    if (rt + 1 < n_rt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces
+    if (st + 1 < n_st) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage's pieces
   }
 }
 
@@ -197,18 +205,29 @@ int launch_splitk(const ZmiGemvArgs& a, int epi, float* part, const void* ln_w, 
   const int n_rt = (a.M + RT - 1) / RT, target = zmi_option(ZMI_OPT_SPLITK_WGS);
   const int n_rg = std::max(1, std::min(n_rt, target / (n_cb * S::NSEG)));
   const int rpg = (n_rt + n_rg - 1) / n_rg;
-  const size_t lds = 2 * (size_t)S::TILE_BYTES;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, false>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  static const hipError_t attr_dn = hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, true>),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  ZMI_CHECK(attr);
-  ZMI_CHECK(attr_dn);
+  const bool multi = zmi_option(ZMI_OPT_SPLITK_STAGE) != 0;
+  const size_t lds = 2 * (size_t)(multi ? S::RTS : 1) * S::TILE_BYTES;
+  // once per instantiation: allow the stage buffers' dynamic LDS
+  static const hipError_t attr[4] = {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, false, 1>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::TILE_BYTES),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, true, 1>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::TILE_BYTES),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, false, S::RTS>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::RTS * S::TILE_BYTES),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&splitk_kernel<K, true, S::RTS>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 2 * S::RTS * S::TILE_BYTES)};
+  for (hipError_t e : attr) ZMI_CHECK(e);
   const dim3 grid(n_cb * S::NSEG * ((n_rt + rpg - 1) / rpg));
-  if (zmi_option(ZMI_OPT_GEMM_ROWS) & 2)
-    hipLaunchKernelGGL((splitk_kernel<K, true>), grid, dim3(DNT), lds, s, a, part, n_cb, rpg);
+  const bool dn = zmi_option(ZMI_OPT_GEMM_ROWS) & 2;
+  if (dn && multi)
+    hipLaunchKernelGGL((splitk_kernel<K, true, S::RTS>), grid, dim3(DNT), lds, s, a, part, n_cb, rpg);
+  else if (dn)
+    hipLaunchKernelGGL((splitk_kernel<K, true, 1>), grid, dim3(DNT), lds, s, a, part, n_cb, rpg);
+  else if (multi)
+    hipLaunchKernelGGL((splitk_kernel<K, false, S::RTS>), grid, dim3(NT), lds, s, a, part, n_cb, rpg);
   else
-    hipLaunchKernelGGL((splitk_kernel<K, false>), grid, dim3(NT), lds, s, a, part, n_cb, rpg);
+    hipLaunchKernelGGL((splitk_kernel<K, false, 1>), grid, dim3(NT), lds, s, a, part, n_cb, rpg);
   ZMI_CHECK(hipGetLastError());
   if (ln_w) {
     hipLaunchKernelGGL(splitk_reduce_ln_kernel<S::NSEG>, dim3(a.M), dim3(256), 0, s, part, a.M, (bf16_t*)a.out, a.ldo,

@@ -21,7 +21,7 @@ extern "C" const char* zmi_last_error(void) { return g_err; }
 extern "C" int zmi_version(void) { return 3; }
 
 // launch-geometry knobs (speed only: no option changes a result bit); defaults in the table
-static int g_opts[ZMI_OPT_COUNT] = {1, 3, 3, 0, 1, 8, 2, 1, 1, 0, 1, 256, 5, 29, 128, 0, 256};
+static int g_opts[ZMI_OPT_COUNT] = {1, 3, 3, 0, 1, 8, 2, 1, 1, 0, 1, 256, 5, 29, 128, 0, 256, 1};
 int zmi_option(int which) { return (which >= 0 && which < ZMI_OPT_COUNT) ? g_opts[which] : 0; }
 extern "C" int zmi_set_option(int which, int value) {
   if (which < 0 || which >= ZMI_OPT_COUNT) return zmi_fail_msg("zmi_set_option: unknown option");
