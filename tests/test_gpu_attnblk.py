@@ -149,21 +149,25 @@ def test_attn_block_refuses_positions_past_its_reach(slices):
     assert int(err[0].item()) != 0
 
 
-@pytest.mark.parametrize("positions", [
-    (591, 592),                                 # C2 mean position, one slot
-    (0, 1),
-    (127, 128, 511, 512, 900, 1023),            # chunk / block edges and the form's last position
-    (5, -1, 300, 301, 63, 64, 700, 1000),       # 8 rows (the fused forms' default limit), an inactive row
-    (5, -1, 300, 301, 63, 64, 700, -1, 1000, 1001, 31, 32, 255, 256, 900, 17),  # 16 rows
+@pytest.mark.parametrize("positions,chunks", [
+    ((591, 592), 8),                                 # C2 mean position, one slot
+    ((0, 1), 8),
+    ((127, 128, 511, 512, 900, 1023), 8),            # chunk / block edges and the form's last position
+    ((5, -1, 300, 301, 63, 64, 700, 1000), 8),       # 8 rows (the fused forms' default limit), an inactive row
+    ((5, -1, 300, 301, 63, 64, 700, -1, 1000, 1001, 31, 32, 255, 256, 900, 17), 8),  # 16 rows
+    ((1024, 1025), 24),                              # the 24-chunk form: batch-1 steps past the 8-chunk reach
+    ((1161, 1162), 24),
+    ((2661, -1), 24),
+    ((3071, 2047, 1535, 1536), 24),                  # the form's last position, block edges
 ])
-def test_attn_block_oproj_bit_identical_to_separate_launches(positions):
-    """zmi_attn_block_oproj (the 8-chunk split form with the layer's out_proj GEMV in the same launch, its input
-    gathered from the merging workgroups' granules): q, K / V, the attention output and the new residual rows
-    bit-identical to the QKV GEMV + attention + out_proj GEMV (EPI_RESIDUAL) launches; run twice (the second launch
-    finds its own granules from the first: equal values, equal tags)."""
+def test_attn_block_oproj_bit_identical_to_separate_launches(positions, chunks):
+    """zmi_attn_block_oproj (a chunk-split form, 8 or 24 chunk workgroups, with the layer's out_proj GEMV in the same
+    launch, its input gathered from the merging workgroups' granules): q, K / V, the attention output and the new
+    residual rows bit-identical to the QKV GEMV + attention + out_proj GEMV (EPI_RESIDUAL) launches; run twice (the
+    second launch finds its own granules from the first: equal values, equal tags)."""
     L = _lib()
-    slices = 8 | SPLIT
-    st = _setup(positions, 2056, seed=80)
+    slices = chunks | SPLIT
+    st = _setup(positions, 2056 if chunks == 8 else 3080, seed=80)
     R = st["R"]
     ref_q, ref_k, ref_v, ref_out = _separate(st)
     Wo = pack(rnd(D, H * HD, scale=0.03, seed=81))[0]

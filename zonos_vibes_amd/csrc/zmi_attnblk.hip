@@ -38,7 +38,9 @@ static_assert(QG * QW == DNW, "both roles run the same block size");
 constexpr int XG = 4;                         // query heads per kv head
 constexpr int QKV_GRAN = (XG + 2) * HD / 2;   // q pairs | k pairs | v pairs per (row, kv head)
 constexpr int XC_CH_MAX = 24;                 // widest chunk-split form (chunk workgroups per unit)
-constexpr int XC_WORDS_MAX = 3 * XC_CH_MAX * XG + XC_CH_MAX * XG * HD;  // its granules (layout below)
+// its granules (layout below: maxima, l, M_j, P.V partials), then the fused out_proj role's output granules and
+// merge flags
+constexpr int XC_WORDS_MAX = 3 * XC_CH_MAX * XG + XC_CH_MAX * XG * HD + XG * HD / 2 + HD / 16;
 // + the score granules [XG][DS_KEYS] of the score-exchange forms, or the chunk-split form's granules
 constexpr int GRAN_STRIDE = QKV_GRAN + (XG * DS_KEYS > XC_WORDS_MAX ? XG * DS_KEYS : XC_WORDS_MAX);
 constexpr int NT = DNW * 64;
@@ -774,7 +776,7 @@ struct XcG {
   static constexpr int GM = 0, GL = GM + XCH * XG, GB = GL + XCH * XG, GO = GB + XCH * XG;
   static constexpr int WORDS = GO + XCH * XG * HD;
   // the fused out_proj role (OPROJ): the unit's output as XG HD / 2 {bf16 pair, tag} granules, then one flag per
-  // merging workgroup, after the chunk granules (only the 8-chunk form leaves room for them in the unit's area)
+  // merging workgroup, after the chunk granules
   static constexpr int OG = WORDS, OF = OG + XG * HD / 2, OWORDS = OF + HD / 16;
   static constexpr bool OPROJ_FITS = QKV_GRAN + OWORDS <= GRAN_STRIDE;
   static_assert(WORDS <= GRAN_STRIDE - QKV_GRAN, "the chunk-split granules fit the unit's area");
@@ -1122,7 +1124,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
 // PRO: the projection's prologue, LayerNorm (transformer blocks) or ADDLN (the hybrid's MHA blocks:
 // layer_norm_fn(hidden, residual) with the new residual written by column block 0). SELF: the
 // attention role is xr_body (self-scoring) instead of xs_body (score exchange).
-// OPROJ (chunk-split form, 8 chunks): a fourth role after the attention workgroups runs the layer's out_proj GEMV
+// OPROJ (chunk-split forms, 8 or 24 chunks): a fourth role after the attention workgroups runs the layer's out_proj GEMV
 // (_torch.py:115,140 + the residual :100), its weights loaded at its start and its activation rows gathered from the
 // merging workgroups' output granules (zmi_gemv_impl.h FUSE 3), so out_proj needs no launch of its own.
 template <int S, int PRO, int FORM, bool OPROJ>
@@ -1242,16 +1244,20 @@ int attn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, uns
   const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
   if (form == FORM_SPLIT ? (sl != 8 && sl != 24) : (sl != 4 && sl != 8))
     return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 or 24 | ZMI_ATTNBLK_SPLIT");
-  if (oproj) {  // the out_proj role (8-chunk split form, LayerNorm'd transformer blocks)
+  if (oproj) {  // the out_proj role (split forms, LayerNorm'd transformer blocks)
     const ZmiGemvArgs& o = *oproj;
-    if (form != FORM_SPLIT || sl != 8 || addln)
-      return zmi_fail_msg("attn_block: the fused out_proj runs with the 8-chunk split form and a LayerNorm prologue");
+    if (form != FORM_SPLIT || addln)
+      return zmi_fail_msg("attn_block: the fused out_proj runs with the chunk-split forms and a LayerNorm prologue");
     if (o.K != a.hq * a.hd || o.N % (8 * QG) || o.n_valid != o.N || o.M != a.M || o.ln_w || o.pro != ZMI_PRO_AUTO ||
         !o.out || o.ldo % 8 || o.ldo < o.N || o.X != attn_out)
       return zmi_fail_msg("attn_block: out_proj must be the plain residual GEMV over the attention output "
                           "(K = hq hd, N % 16 == 0, same rows, X = attn_out)");
-    ZMI_CHECK((launch_block<8, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s,
-                                                                   oproj)));
+    if (sl == 8)
+      ZMI_CHECK((launch_block<8, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s,
+                                                                     oproj)));
+    else
+      ZMI_CHECK((launch_block<24, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf,
+                                                                      s, oproj)));
     return 0;
   }
 #define ZMI_BLK(S_, P_, F_) launch_block<S_, P_, F_>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)

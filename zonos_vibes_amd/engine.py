@@ -141,6 +141,8 @@ class HipEngine:
         # during the attention chain and gather the attention output from the merging workgroups' granules, so
         # no out_proj launch follows (identical bits; the prefetch role then warms only fc1's head)
         self.attn_oproj = True
+        # ... also in the 24-chunk form (batch-1 steps at positions 1024 .. 3071)
+        self.attn_oproj_wide = True
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
         # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
         # device: fc1's weights stream while the out_proj chain runs (identical bits). Off: it loses to the
@@ -600,8 +602,9 @@ class HipEngine:
                                               ctypes.byref(pf), self.sptr), "attn_block")
 
     def _use_attn_oproj(self, form: str) -> bool:
-        """out_proj inside the fused block: the 8-chunk split form of a LayerNorm'd transformer block."""
-        return self.attn_oproj and form == "split" and not self.hybrid and self.H * self.hd == self.d
+        """out_proj inside the fused block: the chunk-split forms (8 and 24 chunks) of a LayerNorm'd transformer block."""
+        wide_ok = form == "split24" and self.attn_oproj_wide
+        return self.attn_oproj and (form == "split" or wide_ok) and not self.hybrid and self.H * self.hd == self.d
 
     def _run_attn_ffn(self, item):
         a, o, f, i = item
