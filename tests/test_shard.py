@@ -125,3 +125,32 @@ def test_gpu_two_ranks_equal_single_process(tmp_path):
         ref = m.generate(conds[i].to("cuda:0"), max_new_tokens=mnt[i], sampling_params=dict(temperature=0.0),
                          progress_bar=False).cpu()
         assert torch.equal(got[i], ref), i
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from zonos_vibes_amd.shard import _gather_collective
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(3)
+        local = [torch.randint(0, 1026, (1, 9, t), generator=g) for t in (7, 1, 33)]
+        got = _gather_collective(local, [2, 0, 1], 3, 0, None, torch.device("cuda", 0), rank, world)
+        torch.save({"local": local, "got": [c.cpu() for c in got]}, os.path.join(out_dir, "rccl.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_int16_gather_path_on_one_gpu(tmp_path):
+    """gather_codes' collective path on RCCL (backend "nccl") with one rank on cuda:0: the size headers and the
+    2-byte code payload go through RCCL all_gathers on the device and come back in global utterance order (the
+    multi-rank path the 8-GPU bench would take; a one-GPU box cannot run two RCCL ranks). This test found that
+    RCCL has no int16 all_gather: the payload now travels as a bfloat16 view of the int16 codes."""
+    port = _free_port()
+    mp.spawn(_rccl_worker, args=(1, port, str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(tmp_path / "rccl.pt", weights_only=True)
+    local, got = r["local"], r["got"]
+    assert [tuple(c.shape) for c in got] == [(1, 9, 1), (1, 9, 33), (1, 9, 7)]
+    assert torch.equal(got[2], local[0]) and torch.equal(got[0], local[1]) and torch.equal(got[1], local[2])

@@ -65,13 +65,18 @@ def gather_codes(local: Sequence[torch.Tensor], local_idx: Sequence[int], n_tota
     Two all_gathers of fixed-shape int64/int16 tensors (sizes, then the padded payload), so it runs
     unchanged on RCCL (device tensors) and gloo (CPU tensors). Returns the full list on `dst`, None
     elsewhere."""
-    import torch.distributed as dist
     rank, world = _rank_world(group)
     if world == 1:
         out: list[torch.Tensor | None] = [None] * n_total
         for i, c in zip(local_idx, local):
             out[i] = c
         return out  # type: ignore[return-value]
+    return _gather_collective(local, local_idx, n_total, dst, group, device, rank, world)
+
+
+def _gather_collective(local, local_idx, n_total, dst, group, device, rank, world):
+    """gather_codes' collective path (any world size, including 1 in tests: the RCCL int16 hand-off on one GPU)."""
+    import torch.distributed as dist
     lens = [int(c.shape[-1]) for c in local]
     meta = torch.tensor([len(local), sum(lens)] + [v for i, t in zip(local_idx, lens) for v in (i, t)],
                         dtype=torch.int64)
@@ -84,8 +89,10 @@ def gather_codes(local: Sequence[torch.Tensor], local_idx: Sequence[int], n_tota
     metas = [torch.zeros_like(meta_p) for _ in range(world)]
     dist.all_gather(metas, meta_p, group=group)
     tmax = max(int(m[1].item()) for m in metas)
-    # int16 payload on RCCL; gloo has no int16 collectives, so it carries int32
-    wire = torch.int16 if dist.get_backend(group) == "nccl" else torch.int32
+    # 2-byte payload on RCCL: the codes as int16 bit patterns, gathered as a bfloat16 view (RCCL / NCCL have no int16
+    # type; all_gather copies bytes, so any 2-byte type carries them exactly); gloo carries int32
+    nccl = dist.get_backend(group) == "nccl"
+    wire = torch.int16 if nccl else torch.int32
     flat = torch.zeros(N_CODEBOOKS, max(tmax, 1), dtype=wire, device=device)
     if local:
         cat = torch.cat([c.reshape(N_CODEBOOKS, -1) for c in local], dim=1)
@@ -93,7 +100,10 @@ def gather_codes(local: Sequence[torch.Tensor], local_idx: Sequence[int], n_tota
             raise ValueError("codes out of the int16 hand-off range [0, 1025]")
         flat[:, :cat.shape[1]] = cat.to(device=device, dtype=wire)
     flats = [torch.zeros_like(flat) for _ in range(world)]
-    dist.all_gather(flats, flat, group=group)
+    if nccl:
+        dist.all_gather([f.view(torch.bfloat16) for f in flats], flat.view(torch.bfloat16), group=group)
+    else:
+        dist.all_gather(flats, flat, group=group)
     if rank != dst:
         return None
     out = [None] * n_total
