@@ -62,7 +62,7 @@ def gather_codes(local: Sequence[torch.Tensor], local_idx: Sequence[int], n_tota
                  group=None, device: torch.device | str = "cpu") -> list[torch.Tensor] | None:
     """End-of-batch gather: every rank's [1, 9, T_i] codes to rank `dst`, in global utterance order.
 
-    Two all_gathers of fixed-shape int64/int16 tensors (sizes, then the padded payload), so it runs
+    Two all_gathers of fixed-shape tensors (int64 sizes, then the padded 2-byte code payload), so it runs
     unchanged on RCCL (device tensors) and gloo (CPU tensors). Returns the full list on `dst`, None
     elsewhere."""
     rank, world = _rank_world(group)
