@@ -629,10 +629,13 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
     torch.cuda.synchronize()
     busy = time.perf_counter() - t0
     g0 = time.perf_counter()
-    gathered = None
+    gathered, gather_err = None, None
     if dist:
         from zonos_vibes_amd.shard import gather_codes
-        gathered = gather_codes(local, mine, n_utt, 0, None, dev)
+        try:
+            gathered = gather_codes(local, mine, n_utt, 0, None, dev)
+        except Exception as exc:  # reported in the line, never fatal to the measurement
+            gather_err = f"{type(exc).__name__}: {exc}"[:200]
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -658,6 +661,8 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
            "lpt_tail": round(max(busys) / (sum(busys) / len(busys)), 3), "gather_ms": round(gather_ms, 1)}
     if rank == 0 and dist:
         res["gathered_utterances"] = len(gathered)
+    if gather_err:
+        res["gather_error"] = gather_err
     return res
 
 
