@@ -660,7 +660,7 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
            "wall_s": round(max(walls), 3), "busy_s_per_rank": [round(b, 3) for b in busys],
            "lpt_tail": round(max(busys) / (sum(busys) / len(busys)), 3), "gather_ms": round(gather_ms, 1)}
     if rank == 0 and dist:
-        res["gathered_utterances"] = len(gathered)
+        res["gathered_utterances"] = len(gathered) if gathered is not None else 0
     if gather_err:
         res["gather_error"] = gather_err
     return res
