@@ -185,6 +185,7 @@ class HipEngine:
         # times, then the one-step graph for the rest; the same launches in the same order). C2 step at position
         # 591: 950.2-950.5 us with 1, 946.8 with 4, 945.8-946.0 with 8, 945.2 with 16 (profiles/r05_graph_steps_ab.jsonl)
         self.graph_steps = 16
+        self.graph_steps_max_slots = 8
         # generate_batch steps only slots 0 .. the highest busy one (bucketed), not every slot
         self.batch_shrink = True
         self.slot_greedy = [False] * self.S
@@ -742,7 +743,10 @@ class HipEngine:
         s = self._rows(slots) // 2
         for k, form in self._segments(n, s):
             if use_graph:
-                u = self.graph_steps
+                # multi-step graphs only for small batches: the many-slot share (C3) captures a graph per busy-slot
+                # bucket inside its timed run, and there the 16-step captures cost more than the replay seams they
+                # save (C3 share 133.9x with 1 step per graph against 132.5-132.7x with 16)
+                u = self.graph_steps if s <= self.graph_steps_max_slots else 1
                 if u > 1 and k >= u:  # runs of u-step graphs, then the remainder one step per replay
                     _lib.check(self.lib.zmi_graph_launch(self.capture(s, form, u), k // u, self.sptr), "graph_launch")
                 if k % u or u <= 1:
