@@ -83,14 +83,6 @@ int zmi_gemv_splitk(const ZmiGemvArgs* args, int epi, float* part, int64_t part_
 int zmi_gemv_splitk_ln(const ZmiGemvArgs* args, int epi, float* part, int64_t part_floats, const void* ln_w,
                        const void* ln_b, float eps, void* xn, int ldxn, void* stream);
 int64_t zmi_gemv_splitk_floats(int M, int N);
-/* Many-row K = 2048 GEMM, K-split pair form (the engine's `rows_pair` route for the launches that
- * zmi_gemv_launch would run as its many-row form: qkv, fc1, heads over > 16 rows; reference _torch.py:114-115,
- * 147-152, model.py:100-101): each 128-column unit runs on two workgroups, one per K half, the upper handing its
- * fp32 segment sums to the lower through `work`. Plain GEMM (ln_w NULL, pro AUTO, groups 0), every epilogue but
- * the fused ones; bit-identical to zmi_gemv_launch for every row. work: zmi_gemv_rows_pair_bytes(M, N) bytes,
- * zeroed once at allocation (each launch leaves its tile counters at zero again). */
-int zmi_gemv_rows_pair(const ZmiGemvArgs* args, int epi, void* work, int64_t work_bytes, void* stream);
-int64_t zmi_gemv_rows_pair_bytes(int M, int N);
 /* out[r] = LayerNorm(x[r]) bf16, r < m (nn.LayerNorm, _torch.py:62: norm_f for the backbone plugin),
  * with the GEMV LayerNorm prologue's arithmetic; k in {512, 1024, 2048, 4096}. */
 int zmi_layernorm_rows(const void* x, int ldx, int m, int k, const void* w, const void* b, float eps, void* out,

@@ -2,8 +2,6 @@
 
     python tools/gemm_rows_bench.py [rows,...] [ZMI_OPT_GEMM_ROWS values,...]
 
-(option value -1: the K-split pair form, zmi_gemv_rows_pair)
-
 For each row count and the Zonos-v0.1 K = 2048 shapes (qkv 3072, out_proj 2048, fc1 16384 SwiGLU-packed, heads
 9248): zmi_gemv_launch over 8 weight copies in turn (so weights come from HBM, as in a decode step), each form
 checked bit-identical to the first. One JSON line per (shape, rows, option): us per launch, weight GB/s.
@@ -38,19 +36,14 @@ def main():
             out = torch.zeros(M, N, dtype=torch.float32, device=dev)
             ref = None
             for o in opts:
-                _lib.check(lib.zmi_set_option(_lib.OPT_GEMM_ROWS, max(o, 3) if o < 0 else o))
-                work = torch.zeros(max(lib.zmi_gemv_rows_pair_bytes(M, N), 16), dtype=torch.uint8, device=dev)
+                _lib.check(lib.zmi_set_option(_lib.OPT_GEMM_ROWS, o))
                 args = []
                 for W in Ws:
                     a = _lib.GemvArgs()
                     a.W, a.X, a.M, a.N, a.K, a.ldx = W.data_ptr(), X.data_ptr(), M, N, K, K
                     a.out, a.ldo, a.n_valid, a.eps = out.data_ptr(), N, N, 1e-5
                     args.append(a)
-                if o < 0:
-                    run = lambda: [_lib.check(lib.zmi_gemv_rows_pair(ctypes.byref(a), _lib.EPI_F32, work.data_ptr(),  # noqa
-                                                                     work.numel(), sp)) for a in args]
-                else:
-                    run = lambda: [_lib.check(lib.zmi_gemv_launch(ctypes.byref(a), _lib.EPI_F32, sp)) for a in args]  # noqa
+                run = lambda: [_lib.check(lib.zmi_gemv_launch(ctypes.byref(a), _lib.EPI_F32, sp)) for a in args]  # noqa
                 with torch.cuda.stream(s):
                     run()
                     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

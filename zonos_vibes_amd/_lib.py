@@ -139,8 +139,6 @@ _SIGS = {
     "zmi_attn_block_gran_words": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
     "zmi_gemv_splitk_floats": (c_int64, [c_int, c_int]),
-    "zmi_gemv_rows_pair": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p]),
-    "zmi_gemv_rows_pair_bytes": (c_int64, [c_int, c_int]),
     "zmi_gemv_splitk_ln": (c_int, [ctypes.POINTER(GemvArgs), c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float,
                                    c_void_p, c_int, c_void_p]),
     "zmi_attn_block_pf": (c_int, [ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -20,7 +20,7 @@ DIAG_LIB = os.path.join(HERE, "libzonos_diag.so")
 SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + ["zmi_attn.hip", "zmi_attnblk.hip", "zmi_sample.hip",
                                                                         "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip",
                                                                         "zmi_mamba.hip", "zmi_mambablk.hip",
-                                                                        "zmi_gemm_splitk.hip", "zmi_gemm_pair.hip"]
+                                                                        "zmi_gemm_splitk.hip"]
 DIAG_SOURCES = ["zmi_ffnblk.hip", "zmi_attnffn.hip", "zmi_engine.hip", "zmi_layer.hip"]
 HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_attn_merge.h", "zmi_attn_ds.h", "zmi_mamba_step.h",
            "zmi_prefetch.h", "zmi_engine.h"]

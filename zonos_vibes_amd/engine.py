@@ -186,9 +186,6 @@ class HipEngine:
         # 591: 950.2-950.5 us with 1, 946.8 with 4, 945.8-946.0 with 8, 945.2 with 16 (profiles/r05_graph_steps_ab.jsonl)
         self.graph_steps = 16
         self.graph_steps_max_slots = 8
-        # the many-row K = 2048 GEMMs (qkv, fc1, heads over > 16 rows) as K-split CU pairs (zmi_gemv_rows_pair: each
-        # CU reads half of every activation row; identical bits)
-        self.rows_pair = False
         # generate_batch steps only slots 0 .. the highest busy one (bucketed), not every slot
         self.batch_shrink = True
         self.slot_greedy = [False] * self.S
@@ -257,9 +254,6 @@ class HipEngine:
             self.eng_gran = self.lay_gran = self.ffn_gran = self.attn_gran = None
             # zmi_gemv_splitk's fp32 segment sums (fc2 / out_proj over many rows: decode and prefill)
             self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
-            # zmi_gemv_rows_pair's hand-off and tile counters (zeroed once; every launch leaves the counters at zero)
-            pair_n = max(2 * self.F, HEADS_N_PAD, (self.H + 2 * self.Hkv) * self.hd)
-            self.pair_work = z(self.lib.zmi_gemv_rows_pair_bytes(max(R, self.pre_rows), pair_n), dt=torch.uint8)
             self.samp_cnt = z(S, dt=torch.int32)
             self.next_tok = z(S, N_CODEBOOKS, dt=torch.int32)
             self.st = {k: z(S, dt=torch.int32) for k in
@@ -358,18 +352,7 @@ class HipEngine:
             _lib.check(self.lib.zmi_gemv_splitk(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
                                                 self.splitk_part.numel(), self.sptr), "gemv_splitk")
             return
-        if self.rows_pair and self._use_pair(a, epi):
-            _lib.check(self.lib.zmi_gemv_rows_pair(ctypes.byref(a), epi, self.pair_work.data_ptr(),
-                                                   self.pair_work.numel(), self.sptr), "gemv_rows_pair")
-            return
         _lib.check(self.lib.zmi_gemv_launch(ctypes.byref(a), epi, self.sptr), "gemv")
-
-    def _use_pair(self, a, epi) -> bool:
-        """The launches zmi_gemv_launch runs as its many-row form (zmi_gemv_impl.h rows_form), with room in pair_work."""
-        rows_form = a.M > 64 or (a.M > 32 and a.N >= 3072) or a.N >= 8192
-        return (a.K == 2048 and a.M > 16 and rows_form and not a.ln_w and a.pro == _lib.PRO_AUTO and a.groups == 0
-                and epi in (_lib.EPI_STORE, _lib.EPI_RESIDUAL, _lib.EPI_QKV, _lib.EPI_SWIGLU, _lib.EPI_LOGITS, _lib.EPI_F32)
-                and self.lib.zmi_gemv_rows_pair_bytes(a.M, a.N) <= self.pair_work.numel())
 
     def _use_splitk(self, a, epi) -> bool:
         lo = {8192: self.splitk_rows, 2048: self.splitk_o_rows, 4096: self.splitk_m_rows}.get(a.K, 0)
