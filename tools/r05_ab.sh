@@ -8,6 +8,8 @@
 #             differ in fp32 rounding), its kernel stats
 #   oproj24   the fused out_proj role in the 24-chunk form (engine attn_oproj_wide): tests, the 30 s batch-1 line
 #   pmc_ssd   one PMC pass (LDS / wait counters) over the C4 prefill
+#   pf        the separate attention launch's prefetch workgroups (engine attn_prefetch_blocks 128 / 256 / 384): the
+#             C3 share and a C5-shaped job, arms alternating
 case "$1" in
   dense)
     bash tools/steps.sh \
@@ -32,6 +34,14 @@ case "$1" in
     bash tools/steps.sh \
       "bash tools/gpu.sh tests tests/test_gpu_attnblk.py tests/test_gpu_kernels.py tests/test_gpu_splitk.py -k \"attn_block or production_shapes or splitk\"" \
       "bash tools/gpu.sh ab bench_long.py long_oproj \"'{\\\"attn_oproj_wide\\\": true}'\" \"'{\\\"attn_oproj_wide\\\": false}'\" \"'{\\\"attn_oproj_wide\\\": true}'\"" ;;
+  pf)
+    k=gpurun_out/keep
+    for arm in 256 128 384 256 128 384; do
+      timeout -k 10 300 python -u tools/bench_c3.py "{\"attn_prefetch_blocks\": $arm}" >> $k/c3_pf.jsonl 2>> $k/c3_pf.err || exit $?
+    done
+    for arm in 128 256 128 256; do
+      timeout -k 10 300 python -u tools/bench_c5.py 2000 "{\"attn_prefetch_blocks\": $arm}" >> $k/c5_pf.jsonl 2>> $k/c5_pf.err || exit $?
+    done ;;
   pmc_ssd)
     cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}" || exit 1
     mkdir -p gpurun_out/keep

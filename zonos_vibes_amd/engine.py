@@ -131,8 +131,10 @@ class HipEngine:
         # fused forms' reach): workgroups at the end of its grid read out_proj's weights and the first
         # `attn_prefetch_fc1_mb` MB of fc1's while the chunks exchange maxima and merge (0 blocks = off). C5-shaped
         # job (8 slots, 2000 new frames): 1.776-1.786 ms per step without, 1.749 with 128 workgroups, 1.760-1.765
-        # with 256 (+ 16 MB of fc1: 1.764); C3 sample unchanged (profiles/r04_attn_prefetch_ab.jsonl)
-        self.attn_prefetch_blocks = 128
+        # with 256 (+ 16 MB of fc1: 1.764); C3 sample unchanged (profiles/r04_attn_prefetch_ab.jsonl). Round 5, with
+        # the block-form attention: C3 share 133.39-133.41x with 256 against 132.97-133.06 (128) and 133.15-133.24
+        # (384), C5-shaped job 1.702-1.708 ms either way (profiles/r05_attn_prefetch_c3_c5_ab.jsonl)
+        self.attn_prefetch_blocks = 256
         self.attn_prefetch_fc1_mb = 8
         # what the second range is: "fc1" (its head) or "qkv" (the next layer's QKV weights, the heads' on the
         # last layer: they would have to survive out_proj + fc1 + fc2 in the Infinity Cache)
