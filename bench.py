@@ -62,52 +62,35 @@ def _live_state(model, cond):
     return s_len + lead
 
 
-def time_dominant_kernel(model, cond, reps: int = 3):
-    """The dominant kernel of the C2 step, timed with HIP events on the engine stream inside this run.
-    Engine plan: zmi_layer_engine with the next layer's QKV (layer_engine_kernel<0>: 121.6 MB of weights + the
-    layer's K / V per launch), layers 0..24 back to back at the C2 mean position, every layer's hand-off granules
-    zeroed before each pass (outside the events). Launch plan: the fc1 GEMV (LayerNorm prologue + SwiGLU
-    epilogue, 67.1 MB). The 26 layers' weights (3.2 GB) rotate, so the bytes come from HBM as in the decode step.
-    Returns (us per launch, algorithmic bytes per launch, kernel name)."""
-    e = model.engine
-    pos = _live_state(model, cond)
-    form = e._segments(1, 1)[0][1]
-    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    tot = 0.0
-    if form == "engine":
-        items = [it for kind, it in e._plan(2, form) if kind == "layereng" and it.next == 0]
-
-        def run():
-            for it in items:
-                _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
-        bytes_launch, name = engine_bytes(e, pos), "layer_engine_kernel<0>"
-    else:
-        items = [item for kind, item in e._plan(2, form) if kind == "gemv" and item[1] == _lib.EPI_SWIGLU]
-        assert items, "the C2 plan has no fc1 GEMV launch"
-
-        def run():
-            for it in items:
-                e._run_gemv(it)
-        d, F = e.d, e.F
-        bytes_launch, name = 2 * F * d * 2 + 2 * d * 2 + 2 * d * 2 + 2 * F * 2, "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"
-    with torch.cuda.stream(e.stream):
-        for r in range(reps + 1):
-            if form == "engine":
-                e.lay_gran.zero_()
-            st.record(e.stream)
-            run()
-            en.record(e.stream)
-            en.synchronize()
-            if r:
-                tot += st.elapsed_time(en) * 1000.0
-    e.check_errors()
-    e.release(0)
-    return tot / (reps * len(items)), bytes_launch, name
+# the committed FETCH_SIZE pass of each dominant-kernel candidate, newest round first (tools/gpu.sh round)
+PMC_FILES = {"attn_block_kernel<8, 1, 2, true>": ["r06_pmc_attnblk_fetch.json", "r05_pmc_attnblk_fetch.json"],
+             "attn_block_kernel<24, 1, 2, true>": ["r06_pmc_attnblk24_fetch.json"],
+             "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": ["r06_pmc_fc1_fetch.json", "r05_pmc_fc1_fetch.json"],
+             "gemv_kernel<1, 8, 16, 8, 0, 1, 1>": ["r06_pmc_fc2_fetch.json"]}
 
 
-# the committed FETCH_SIZE pass of each dominant-kernel candidate (tools/gpu.sh round)
-PMC_FILES = {"layer_engine_kernel<0>": "r04_pmc_engine_fetch.json",
-             "gemv_kernel<2, 4, 8, 16, 1, 3, 1>": "r05_pmc_fc1_fetch.json"}
+def roofline_entry(name: str, ent: dict) -> dict:
+    """The bench line's roofline object for one kernel of the C2 step table: algorithmic bytes per launch / its mean
+    launch time (HIP events on the engine stream in this run) against the HBM peak, traffic from the committed
+    FETCH_SIZE pass of the same instantiation."""
+    traffic, src = pmc_traffic(ent["kernel"])
+    return {"kernel": f"{ent['kernel']} ({name})", "bound": "hbm", "achieved": ent["GBps"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ent["GBps"] / HBM_PEAK_GBS, 3), "traffic": traffic,
+            "traffic_source": f"{src} (rocprofv3 FETCH_SIZE x2, bytes/launch)" if src else None,
+            "avg_us": ent["us"], "bytes_per_launch": ent["bytes"], "launches_per_step": ent["launches_per_step"],
+            "us_per_step": round(ent["us"] * ent["launches_per_step"], 1)}
+
+
+def dominant_kernels(ktab: dict) -> tuple[dict, dict | None]:
+    """(dominant, fc1) roofline objects from the C2 step's kernel table: the dominant kernel is the one with the
+    most GPU time per step (launch time x launches per step), as rocprof's --stats ranks it; fc1, the largest
+    weight stream, rides along as a secondary entry."""
+    ks = {k: v for k, v in ktab["kernels"].items() if "bytes" in v and "GBps" in v and "kernel" in v}
+    if not ks:
+        return None, None
+    dom = max(ks, key=lambda k: ks[k]["us"] * ks[k]["launches_per_step"])
+    fc1 = next((k for k in ks if k.startswith("fc1")), None)
+    return roofline_entry(dom, ks[dom]), (roofline_entry(fc1, ks[fc1]) if fc1 and fc1 != dom else None)
 
 
 def _time_fused(e, items, gran, run, reps: int) -> float:
@@ -130,19 +113,19 @@ def _time_fused(e, items, gran, run, reps: int) -> float:
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of the dominant kernel from the committed FETCH_SIZE pass of THIS kernel
-    (tools/gpu.sh round: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py fc1, x2 gfx950
-    correction; a counter pass serialises dispatches, so it is not repeated inside the timed run). None
-    when the profile is absent or measured another kernel."""
-    name = PMC_FILES.get(kernel)
-    path = os.path.join(REPO, "profiles", name) if name else None
-    if not path or not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        d = json.load(f)
-    if not d.get("kernels") or any(kernel not in k for k in d["kernels"]):
-        return None, None
-    return int(d["FETCH_SIZE_bytes_per_launch"]), f"profiles/{name}"
+    """HBM bytes per launch of a kernel from the newest committed FETCH_SIZE pass of THIS instantiation
+    (tools/gpu.sh round: rocprofv3 --pmc FETCH_SIZE over tools/pmc_driver.py, x2 gfx950 correction; a counter
+    pass serialises dispatches, so it is not repeated inside the timed run). (None, None) when no profile of
+    that instantiation is committed."""
+    for name in PMC_FILES.get(kernel, []):
+        path = os.path.join(REPO, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("kernels") and all(kernel in k for k in d["kernels"]):
+            return int(d["FETCH_SIZE_bytes_per_launch"]), f"profiles/{name}"
+    return None, None
 
 
 def time_decode_step(model, cond, steps: int = 64, n_new: int = N_NEW, at: int | None = None):
@@ -191,17 +174,19 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     gem = [it for kd, it in plan if kd == "gemv"]
     res = [it for it in gem if it[1] == _lib.EPI_RESIDUAL]
     fused_ffn = any(kd == "ffnblk" for kd, _ in plan)
-    kinds = {
-        "out_proj": ([it for it in res if it[0].K == e.H * e.hd and not fused_ffn], d * d * 2),
-        "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2),
-        "fc2": ([it for it in res if it[0].K == F], d * F * 2),
-        "heads (LN + logits)": ([it for it in gem if it[1] == _lib.EPI_LOGITS], 9 * 1025 * d * 2),
+    kinds = {  # name: (launch items, algorithmic bytes per launch, rocprof instantiation)
+        "out_proj": ([it for it in res if it[0].K == e.H * e.hd and not fused_ffn], d * d * 2, "gemv_kernel (out_proj)"),
+        "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2,
+                              "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"),
+        "fc2": ([it for it in res if it[0].K == F], d * F * 2, "gemv_kernel<1, 8, 16, 8, 0, 1, 1>"),
+        "heads (LN + logits)": ([it for it in gem if it[1] == _lib.EPI_LOGITS], 9 * 1025 * d * 2,
+                                "gemv_kernel<2, 4, 8, 16, 1, 4, 1>"),
     }
     kinds = {k: v for k, v in kinds.items() if v[0]}
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {}
     with torch.cuda.stream(e.stream):
-        for name, (items, nbytes) in kinds.items():
+        for name, (items, nbytes, kname) in kinds.items():
             for it in items:
                 e._run_gemv(it)
             st.record(e.stream)
@@ -212,7 +197,8 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
             en.synchronize()
             us = st.elapsed_time(en) * 1000.0 / (reps * len(items))
             out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
-                             hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items))
+                             hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items),
+                             kernel=kname)
         ffn = [it for kd, it in plan if kd == "ffnblk"]
         if ffn:
             us = _time_fused(e, ffn, e.ffn_gran, e._run_ffn_block, reps)
@@ -228,9 +214,13 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
             what = "LN + QKV + RoPE + KV write + attention" + (" + out_proj + residual" if oproj else "")
             note = ("QKV and out_proj weights + the layer's K/V of both rows; the launch also prefetches fc1's head"
                     if oproj else "QKV weights + the layer's K/V of both rows; the launch also prefetches out_proj's weights")
+            sl = blk[0][3]
+            fm = 2 if sl & _lib.ATTNBLK_SPLIT else (1 if sl & _lib.ATTNBLK_SELF else 0)
+            kname = f"attn_block_kernel<{sl & 255}, 1, {fm}, {'true' if oproj else 'false'}>"
             out[f"attn_block ({form}: {what})"] = dict(
                 us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
-                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk), note=note)
+                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk), note=note,
+                kernel=kname)
         # the sampler launches captured in one graph: a Python-side launch costs more than the kernel, so
         # back-to-back launches from the host would time the host
         n_s = 8 * reps
@@ -629,13 +619,12 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
     torch.cuda.synchronize()
     busy = time.perf_counter() - t0
     g0 = time.perf_counter()
-    gathered, gather_err = None, None
+    gathered = None
     if dist:
+        # a failure here is fatal: a rank that raises leaves the others inside a collective, so the run ends and
+        # torch.distributed.run reports it, rather than the ranks meeting at a barrier that never completes
         from zonos_vibes_amd.shard import gather_codes
-        try:
-            gathered = gather_codes(local, mine, n_utt, 0, None, dev)
-        except Exception as exc:  # reported in the line, never fatal to the measurement
-            gather_err = f"{type(exc).__name__}: {exc}"[:200]
+        gathered = gather_codes(local, mine, n_utt, 0, None, dev)
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -661,8 +650,6 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
            "lpt_tail": round(max(busys) / (sum(busys) / len(busys)), 3), "gather_ms": round(gather_ms, 1)}
     if rank == 0 and dist:
         res["gathered_utterances"] = len(gathered) if gathered is not None else 0
-    if gather_err:
-        res["gather_error"] = gather_err
     return res
 
 
@@ -784,6 +771,60 @@ def _dac_weights_cpu():
     return dict(syn.iter_torch_cpu(syn.dac_specs(), 0))
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher around it: run N ranks of this same command line under
+    torch.distributed.run (127.0.0.1 rendezvous, a free port) as a child process; returns its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """The multi-rank harness without a GPU (gloo, CPU tensors): the C3 set's LPT plan over `world` ranks
+    (shard.lpt_assign, as time_c3_sharded uses it), a stand-in generator that emits placeholder codes of each
+    utterance's length (no kernel, no oracle: this checks the plumbing, not the decode), the barrier-bracketed
+    timing reduced as the max over ranks, and the end-of-batch gather (shard.gather_codes) to rank 0. Rank 0
+    prints one JSON line with the world it saw and the gathered utterance count."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from zonos_vibes_amd.shard import gather_codes, lpt_assign
+    dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=5))
+    try:
+        per_gpu = 8
+        lcs, n_all = c3_job()
+        n_utt = min(len(lcs), per_gpu * world)
+        costs = [n + 8 + lc + 1 for lc, n in zip(lcs[:n_utt], n_all[:n_utt])]
+        mine = lpt_assign(costs, world)[rank]
+        dist.barrier()
+        t0 = time.perf_counter()
+        local = [torch.full((1, 9, n_all[i]), i % 1024, dtype=torch.long) for i in mine]
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fr = torch.tensor([sum(int(c.shape[-1]) for c in local)], dtype=torch.float64)
+        dist.all_reduce(fr)
+        got = gather_codes(local, mine, n_utt, 0)
+        if rank == 0:
+            ok = got is not None and all(int(c[0, 0, 0]) == i % 1024 and c.shape[-1] == n_all[i] for i, c in enumerate(got))
+            print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                              "backend": "gloo", "wall_s_max_over_ranks": round(float(t.item()), 6),
+                              "c3_sharded": {"utterances": n_utt, "frames": int(fr.item()),
+                                             "gathered_utterances": 0 if got is None else len(got),
+                                             "gathered_in_order": bool(ok)}}), flush=True)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -796,17 +837,31 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (voice clone, 60 s, 8 slots) line in `widened`")
     ap.add_argument("--no-default-cap", action="store_true",
                     help="skip the line with the engine sized for the reference default max_new_tokens")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU / gloo rehearsal of the multi-rank harness (launcher, world check, LPT plan of the C3 "
+                         "set, timing reductions, end-of-batch gather) with placeholder codes; runs no kernel")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start the N ranks as a child torch.distributed.run (this parent touches no GPU) and
+        # exit with its status
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_run:
+        return dry_run(args, rank, world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # rank 0 alone runs the widened lines; the other ranks wait at the next barrier for that long
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(minutes=45))
 
     from zonos_vibes_amd.model import Zonos
     cfg = zonos_v01_transformer()
@@ -861,20 +916,17 @@ def main():
     gather = None
     if dist:
         from zonos_vibes_amd.shard import gather_codes
-        try:
-            g0 = time.perf_counter()
-            got = gather_codes([codes], [rank], world, device=dev)
-            torch.cuda.synchronize()
-            gather = {"ok": True, "ms": round((time.perf_counter() - g0) * 1e3, 2)}
-            if rank == 0:
-                gather["frames_gathered"] = int(sum(c.shape[-1] for c in got))
-        except Exception as exc:  # reported, never fatal to the measurement
-            gather = {"ok": False, "error": f"{type(exc).__name__}: {exc}"[:200]}
+        g0 = time.perf_counter()  # fatal on failure (see time_c3_sharded)
+        got = gather_codes([codes], [rank], world, device=dev)
+        torch.cuda.synchronize()
+        gather = {"ok": True, "ms": round((time.perf_counter() - g0) * 1e3, 2)}
+        if rank == 0:
+            gather["frames_gathered"] = int(sum(c.shape[-1] for c in got))
 
     # kernel-level measurement (outside the timed region)
-    us, bl, dom_name = time_dominant_kernel(model, cond)
     step_us, step_pos = time_decode_step(model, cond)
     ktab = kernel_table(model, cond)
+    roof, roof_fc1 = dominant_kernels(ktab)
     widened = time_widened_rows(model, dev)
     if rank == 0 and not args.no_default_cap:
         widened["default_capacity"] = time_default_capacity(dev, n_new, ref_codes)
@@ -890,8 +942,6 @@ def main():
         c3 = time_c3_sharded(model, dev, rank, world, dist)  # last: grows the engine to 64 slots
     out = None
     if rank == 0:
-        achieved = bl / (us * 1e-6) / 1e9
-        traffic, traffic_src = pmc_traffic(dom_name)
         out = {
             "metric": "real-time factor (44kHz audio s/compute s) + DAC tokens/s/GPU, Zonos-transformer",
             "value": round(rtf, 3), "unit": "x realtime (audio s / wall s, all GPUs)",
@@ -908,13 +958,8 @@ def main():
             "frames_per_s_per_gpu": round(frames / elapsed / world, 1),
             "decode_step_us": round(step_us, 1), "decode_step_pos": step_pos,
             "decode_step_hbm_frac": round(step_bytes(model, step_pos) / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
-            "roofline": {"kernel": dom_name + (" (one whole decode layer + the next layer's QKV: 121.6 MB bf16 weights "
-                                                "+ the layer's K / V per launch)" if "engine" in dom_name else
-                                                " (fc1: LayerNorm prologue + packed SwiGLU epilogue, 67.1 MB)"),
-                         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
-                         "traffic_source": f"{traffic_src} (rocprofv3 FETCH_SIZE x2, bytes/launch)",
-                         "avg_us": round(us, 2), "bytes_per_launch": bl},
+            "roofline": roof,
+            "roofline_fc1": roof_fc1,
             "codes_sha256_16": codes_sha,
             "c2_step_kernels": ktab,
             "utterance_breakdown": breakdown,

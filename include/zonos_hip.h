@@ -8,7 +8,10 @@
  *   - every pointer is a device pointer owned by the caller (allocated by torch), unless noted;
  *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
  *   - every function returns 0 on success or a nonzero status; zmi_last_error() explains it;
- *   - no function allocates or synchronises, so every launcher can be hipGraph-captured.
+ *   - no function allocates or synchronises, so every launcher can be hipGraph-captured;
+ *   - gfx950 only: several launchers size their workgroups for its 160 KB of LDS (the SSD prefill scan ~148 KB, the
+ *     staged split-K GEMM ~132 KB, the DAC's staged convs up to 156 KB) and return an error, with no smaller-LDS
+ *     fallback, where the device grants less.
  */
 #ifndef ZONOS_HIP_H
 #define ZONOS_HIP_H
@@ -364,6 +367,9 @@ int zmi_graph_launch(void* graph_exec, int times, void* stream);
 int zmi_graph_destroy(void* graph_exec);
 
 const char* zmi_last_error(void);
+/* ABI version, bumped whenever a weight layout or an option's meaning changes: 4 = channel-blocked DAC conv weights
+ * [tap][ci / 32][co][32] (zmi_dac_conv / conv_t / conv_out) and the round-5 ZMI_OPT_GEMM_ROWS bits. Check it
+ * before packing weights (zonos_vibes_amd/_lib.py refuses a library whose version differs). */
 int zmi_version(void);
 /* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
  *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the

@@ -213,6 +213,7 @@ DIAG_EXPORTED = sorted(_DIAG_SIGS)
 DIAG_PATH = os.path.join(HERE, "libzonos_diag.so")
 _lib = None
 _diag = None
+ABI_VERSION = 4  # zmi_version() of the library this binding (and its weight packers) is written for
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -226,6 +227,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib_, name)
         fn.restype = res
         fn.argtypes = args
+    if lib_.zmi_version() != ABI_VERSION:  # weight layouts and option meanings change with the version
+        raise RuntimeError(f"{path} has ABI version {lib_.zmi_version()}, this binding expects {ABI_VERSION}: rebuild it")
     return lib_
 
 

@@ -1127,6 +1127,11 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
 // OPROJ (chunk-split forms, 8 or 24 chunks): a fourth role after the attention workgroups runs the layer's out_proj GEMV
 // (_torch.py:115,140 + the residual :100), its weights loaded at its start and its activation rows gathered from the
 // merging workgroups' output granules (zmi_gemv_impl.h FUSE 3), so out_proj needs no launch of its own.
+// Ordering rule: this role writes the residual rows x in place while the same launch's QKV role reads x for its
+// LayerNorm. That is safe because it stores a row only after gathering that row's attention output, which exists
+// only after every QKV column block feeding the row's units has published its granules (each QKV block feeds
+// some (row, kv head) unit that the gather waits on), i.e. after every QKV workgroup has read x. Rows with
+// position < 0 run no attention, so the role neither waits on them nor stores them (act_rows).
 template <int S, int PRO, int FORM, bool OPROJ>
 __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, int n_cb, int n_qkv, const AttnArgs at,
                                                         int n_units, uint64_t* gran, const ZmiPrefetch pf, int n_pf,

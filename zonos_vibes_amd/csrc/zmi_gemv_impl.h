@@ -133,7 +133,7 @@ struct QkvFuse {
 template <int EPI, int RT, int FUSE, class ColSum>
 __device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& colsum, int lane, int rows, int row0,
                                          int g, const uint32_t (&res_pre)[(8 * RT + 63) / 64], int q_pos, int q_kvr,
-                                         const QkvFuse& fz) {
+                                         const QkvFuse& fz, unsigned act_rows = ~0u) {
   constexpr int NE = (8 * RT + 63) / 64;
   const int col0 = g * 8;
   if (EPI == ZMI_EPI_STORE && FUSE == 2) {
@@ -157,7 +157,7 @@ __device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& col
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
       const int e = lane + 64 * i, r = e >> 3, c = e & 7, n = col0 + c;
-      if (r >= rows || n >= a.n_valid) continue;
+      if (r >= rows || n >= a.n_valid || !((act_rows >> r) & 1u)) continue;  // act_rows: FUSE 3's rows with pos >= 0
       const float v = colsum(c, r);
       const size_t m = (size_t)(row0 + r);
       if (EPI == ZMI_EPI_F32) {
@@ -277,6 +277,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   constexpr int NE = (8 * RT + 63) / 64;
   uint32_t res_pre[NE];
   int q_pos = -1, q_kvr = 0;
+  unsigned act_rows = ~0u;  // FUSE 3: rows whose position is >= 0 (the others ran no attention: no residual store)
 
   // (1) activation rows (+ LayerNorm gamma / beta, first tile only) into LDS by DMA, 1 KiB pieces
   // spread over waves; then the tile's epilogue operands
@@ -347,6 +348,8 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     int* qpos = reinterpret_cast<int*>(red);  // the segment-sum area, free until the MFMA chain
     if (tid < rows) qpos[tid] = fz.pos[row0 + tid];
     __syncthreads();
+    act_rows = 0u;
+    for (int r = 0; r < rows; ++r) act_rows |= (qpos[r] >= 0 ? 1u : 0u) << r;
     // (1') wave 0 polls the merge workgroups' flags of the launch's units (8 per (row, kv head); rows whose position
     // is < 0 run no attention and contribute zero rows), sleeping between sweeps, until every unit has at least one
     // flag up: the merges are then nearly done (64 cheap flags instead of 2048 granules while the attention runs)
@@ -659,7 +662,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
       for (int w = 1; w < W; ++w) v += red[((gi * W + w) * 8 + c) * RT + r];
       return v;
     };
-    epilogue<EPI, RT, FUSE>(a, colsum, lane, rows, row0, g, res_pre, q_pos, q_kvr, fz);  // (6)
+    epilogue<EPI, RT, FUSE>(a, colsum, lane, rows, row0, g, res_pre, q_pos, q_kvr, fz, act_rows);  // (6)
   }
   ZMI_GSTAMP(6);
   // one tile when each weight is read once (NTW: M <= RT, every decode launch): no loop state there
