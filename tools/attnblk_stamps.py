@@ -37,6 +37,7 @@ def main():
     e = m.engine
     e.attn_block_slices = e.attn_self_slices = args.slices
     e.attn_oproj = not args.no_oproj
+    e.attn_forms = tuple(dict.fromkeys([args.form, "split", "split24", "xs"]))  # the probed form first
     with torch.cuda.stream(e.stream):
         e.row_pos[:2] = args.pos
         e.row_kv[:2] = torch.arange(2, dtype=torch.int32, device=dev)

@@ -133,7 +133,7 @@ struct QkvFuse {
 template <int EPI, int RT, int FUSE, class ColSum>
 __device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& colsum, int lane, int rows, int row0,
                                          int g, const uint32_t (&res_pre)[(8 * RT + 63) / 64], int q_pos, int q_kvr,
-                                         const QkvFuse& fz, unsigned act_rows = ~0u) {
+                                         const QkvFuse& fz, unsigned act_rows = ~0u, const float2* rope_pre = nullptr) {
   constexpr int NE = (8 * RT + 63) / 64;
   const int col0 = g * 8;
   if (EPI == ZMI_EPI_STORE && FUSE == 2) {
@@ -191,7 +191,10 @@ __device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& col
       float x0 = bfround(colsum(c, r)), x1 = bfround(colsum(c + 1, r));
       if (n < qcols + kcols) {
         const int d = (n < qcols ? n : n - qcols) % a.hd;
-        const float2 cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
+        // rope_pre: the cos / sin pair loaded by the caller before its LayerNorm (a load here is a memory round trip on
+        // the decode step's critical path)
+        const float2 cs = rope_pre ? *rope_pre
+                                   : *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
         const float co = cs.x, si = cs.y;
         const float r0 = x0 * co - x1 * si;
         const float r1 = x1 * co + x0 * si;
@@ -343,6 +346,17 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   __builtin_amdgcn_sched_barrier(0);
   ZMI_GSTAMP(1);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");  // DMA pieces + epilogue operands landed
+  // single-tile QKV launches (every decode step): the epilogue's RoPE cos / sin pair, issued now that the row's
+  // position has landed, so it arrives under the LayerNorm and the MFMA chain instead of after them
+  float2 rope_cs = {1.f, 0.f};
+  if (EPI == ZMI_EPI_QKV && NTW && ew && (lane >> 2) < rows && q_pos >= 0 && q_pos < a.smax) {
+    const int n = col0 + (lane & 3) * 2, qcols = a.hq * a.hd;
+    if (n < qcols + a.hkv * a.hd) {
+      const int d = (n < qcols ? n : n - qcols) % a.hd;
+      rope_cs = *reinterpret_cast<const float2*>(a.rope + ((size_t)q_pos * (a.hd >> 1) + (d >> 1)) * 2);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (FUSE == 3) {
     // the rows' positions (tags) in LDS first: every later check reads them without a dependent global load
     int* qpos = reinterpret_cast<int*>(red);  // the segment-sum area, free until the MFMA chain
@@ -449,12 +463,18 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
       if (lane == 0) part[task] = v;
     }
     __syncthreads();
+#if defined(ZMI_LN_STAMP) && ZMI_LN_STAMP == 1  // diagnostic builds only (tools/build_attnblk_stamps.sh)
+    ZMI_GSTAMP(7);
+#endif
     for (int task = wave; task < ntask; task += NWV) {
       const float mean = ln_combine<NQ>(part + (task / NQ) * NQ) / (float)K;
       const float v = pass(task, mean, true);
       if (lane == 0) part[RT * NQ + task] = v;
     }
     __syncthreads();
+#if defined(ZMI_LN_STAMP) && ZMI_LN_STAMP == 2
+    ZMI_GSTAMP(7);
+#endif
     for (int task = wave; task < ntask; task += NWV) {
       const int r = task / NQ, q = task - r * NQ;
       const float mean = ln_combine<NQ>(part + r * NQ) / (float)K;
@@ -662,7 +682,8 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
       for (int w = 1; w < W; ++w) v += red[((gi * W + w) * 8 + c) * RT + r];
       return v;
     };
-    epilogue<EPI, RT, FUSE>(a, colsum, lane, rows, row0, g, res_pre, q_pos, q_kvr, fz, act_rows);  // (6)
+    epilogue<EPI, RT, FUSE>(a, colsum, lane, rows, row0, g, res_pre, q_pos, q_kvr, fz, act_rows,
+                            (EPI == ZMI_EPI_QKV && NTW) ? &rope_cs : nullptr);  // (6)
   }
   ZMI_GSTAMP(6);
   // one tile when each weight is read once (NTW: M <= RT, every decode launch): no loop state there
