@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B variants of the fused attention block, built HERE (hipcc cross-compiles gfx950) into zonos_vibes_amd/ab/, which
+# git ignores but gpurun ships: lib<name>.so (the product library with zmi_attnblk.hip rebuilt with the given -D flags)
+# and libstamps_<name>.so (the same with the in-kernel phase stamps, for tools/attnblk_stamps.py).
+#   tools/build_ab.sh <name> [-DFLAG=V ...]
+set -e
+cd "$(dirname "$0")/.."
+name=$1; shift
+python -m zonos_vibes_amd.build > /dev/null
+mkdir -p zonos_vibes_amd/ab /tmp/ab_$name
+CXX="/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Izonos_vibes_amd/csrc"
+$CXX "$@" -c zonos_vibes_amd/csrc/zmi_attnblk.hip -o /tmp/ab_$name/p.o &
+$CXX "$@" -DZMI_ATTN_STAMPS -DZMI_GEMV_STAMPS -c zonos_vibes_amd/csrc/zmi_attnblk.hip -o /tmp/ab_$name/s.o &
+wait
+others=$(ls zonos_vibes_amd/build/*.o | grep -v zmi_attnblk)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others /tmp/ab_$name/p.o -o zonos_vibes_amd/ab/lib$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others /tmp/ab_$name/s.o -o zonos_vibes_amd/ab/libstamps_$name.so
