@@ -53,8 +53,11 @@ def main():
             for kind, item in plan:
                 if kind == "gemv":
                     e._run_gemv(item)
+                elif kind == "attn":
+                    i, apf = item
+                    e._attention(i, e.q, 2, None, e.row_pos, e.smax - 1, e.attn, apf)
                 else:
-                    e._attention(item, e.q, 2, None, e.row_pos, e.smax - 1, e.attn)
+                    item()
         e.stream.synchronize()
     st = buf.view(64, 4096, 8).cpu()
     prev_end = None
@@ -68,8 +71,13 @@ def main():
         end = float(((b[:, 6][b[:, 6] > 0]).max() - t0) / 100.0) if (b[:, 6] > 0).any() else None
         last_start = round(float(rel[:, 0].max()), 2)
         gap = None if prev_end is None else round(float((t0 - prev_end) / 100.0), 2)
+        ends = rel[:, 6][b[:, 6] > 0]
+        q = torch.quantile(ends, torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64)).tolist() if len(ends) else []
+        idx = live.nonzero().flatten()
+        xcd = [round(float(rel[:, 6][(idx % 8 == x) & (b[:, 6] > 0)].median()), 2) for x in range(8)]
         print(json.dumps(dict(launch=name, blocks=int(live.sum()), gap_from_prev_us=gap, last_block_start=last_start,
-                              median_stamps_us=med, last_end_us=round(end, 2) if end is not None else None)))
+                              median_stamps_us=med, last_end_us=round(end, 2) if end is not None else None,
+                              end_p10_p50_p90_p99=[round(v, 2) for v in q], end_median_by_block_mod8=xcd)))
         prev_end = t0 + (end or 0) * 100.0
 
 

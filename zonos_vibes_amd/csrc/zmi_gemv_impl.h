@@ -1003,7 +1003,10 @@ hipError_t launch_p(const ZmiGemvArgs& a, hipStream_t s) {
   if (NTW && zmi_option(ZMI_OPT_GEMV_SPREAD)) {
     // a decode launch streams each weight once: its rate is the number of CUs it keeps busy (one CU
     // pulls ~25 GB/s), so reserve LDS such that at most ceil(blocks / CUs) workgroups share a CU
-    const int64_t per_cu = (blocks + zmi_cu_count() - 1) / zmi_cu_count();
+    // (ZMI_OPT_GEMV_SPREAD > 1 caps the workgroups per CU at that value: an occupancy probe; 2 cost fc1 ~0.85 us per
+    // launch, 3 measured the same as 4, profiles/r06_gemv_spread_ab.jsonl)
+    int64_t per_cu = (blocks + zmi_cu_count() - 1) / zmi_cu_count();
+    if (zmi_option(ZMI_OPT_GEMV_SPREAD) > 1) per_cu = std::min<int64_t>(per_cu, zmi_option(ZMI_OPT_GEMV_SPREAD));
     if (per_cu < 8) lds = std::max(lds, LDS_MAX / (size_t)(per_cu + 1) + 1024);
   }
   if (lds > 64 * 1024) {
