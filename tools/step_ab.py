@@ -41,8 +41,9 @@ def main():
             else:
                 setattr(e, k, v)
         e._build_plan()
-        bench.time_decode_step(m, cond, steps=16)  # warm-up (graph capture)
-        us, pos = bench.time_decode_step(m, cond)
+        at = int(os.environ.get("STEP_AT", "0")) or None  # decode position of the timed window (default: C2's mean)
+        bench.time_decode_step(m, cond, steps=16, at=at)  # warm-up (graph capture)
+        us, pos = bench.time_decode_step(m, cond, at=at)
         codes = m.generate(cond, max_new_tokens=48, sampling_params=dict(temperature=0.0), progress_bar=False)
         same = None if ref is None else bool(torch.equal(codes, ref))
         ref = codes if ref is None else ref
