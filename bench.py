@@ -41,17 +41,6 @@ def cond_tensor(seed: int, d: int, dev, lc: int = LC):
     return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(dev)
 
 
-def engine_bytes(e, pos: int, nxt: int = 0) -> int:
-    """Algorithmic HBM bytes of one zmi_layer_engine launch: the layer's out_proj, fc1 and fc2 weights, the next
-    op's weights (QKV of the next layer, or the heads), this layer's K / V of both CFG rows up to pos, the
-    next layer's K / V row written at pos."""
-    d, F = e.d, e.F
-    qkv_n = (e.H + 2 * e.Hkv) * e.hd
-    w = (d * d + 2 * F * d + d * F) * 2 + (qkv_n * d * 2 if nxt == 0 else 9248 * d * 2)
-    kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)
-    return w + kv + (2 * 2 * e.Hkv * e.hd * 2 if nxt == 0 else 0)
-
-
 def _live_state(model, cond):
     """Prefill slot 0 with the bench conditioning and decode to the C2 mean position; returns the position."""
     from zonos_vibes_amd.engine import SamplingParams
@@ -169,13 +158,10 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
     plan = e._plan(2, form)
     d, F, qkv_n = e.d, e.F, (e.H + 2 * e.Hkv) * e.hd
     kv = 2 * e.Hkv * e.hd * 2 * 2 * (pos + 1)  # K + V of both CFG rows, one layer
-    if form == "engine":
-        return _engine_kernel_table(e, plan, pos, reps)
     gem = [it for kd, it in plan if kd == "gemv"]
     res = [it for it in gem if it[1] == _lib.EPI_RESIDUAL]
-    fused_ffn = any(kd == "ffnblk" for kd, _ in plan)
     kinds = {  # name: (launch items, algorithmic bytes per launch, rocprof instantiation)
-        "out_proj": ([it for it in res if it[0].K == e.H * e.hd and not fused_ffn], d * d * 2, "gemv_kernel (out_proj)"),
+        "out_proj": ([it for it in res if it[0].K == e.H * e.hd], d * d * 2, "gemv_kernel (out_proj)"),
         "fc1 (LN + SwiGLU)": ([it for it in gem if it[1] == _lib.EPI_SWIGLU], 2 * F * d * 2,
                               "gemv_kernel<2, 4, 8, 16, 1, 3, 1>"),
         "fc2": ([it for it in res if it[0].K == F], d * F * 2, "gemv_kernel<1, 8, 16, 8, 0, 1, 1>"),
@@ -199,13 +185,6 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
             out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
                              hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items),
                              kernel=kname)
-        ffn = [it for kd, it in plan if kd == "ffnblk"]
-        if ffn:
-            us = _time_fused(e, ffn, e.ffn_gran, e._run_ffn_block, reps)
-            nbytes = (d * d + 2 * F * d) * 2
-            out["ffn_block (out_proj + residual + LN + fc1 + SwiGLU)"] = dict(
-                us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
-                hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(ffn))
         blk = [it for kd, it in plan if kd == "attnblk"]
         if blk:
             us = _time_fused(e, blk, e.blk_gran, e._run_attn_block, reps)
@@ -221,25 +200,9 @@ def kernel_table(model, cond, reps: int = 3) -> dict:
                 us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
                 hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(blk), note=note,
                 kernel=kname)
-        # the sampler launches captured in one graph: a Python-side launch costs more than the kernel, so
-        # back-to-back launches from the host would time the host
-        n_s = 8 * reps
-        _lib.check(e.lib.zmi_graph_begin(e.sptr), "graph_begin")
-        try:
-            for _ in range(n_s):
-                e._sample(e.logits, None, 0, 0, 1)
-        finally:
-            g = ctypes.c_void_p()
-            _lib.check(e.lib.zmi_graph_end(e.sptr, ctypes.byref(g)), "graph_end")
-        _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")  # warm
-        st.record(e.stream)
-        _lib.check(e.lib.zmi_graph_launch(g.value, 1, e.sptr), "graph_launch")
-        en.record(e.stream)
-        en.synchronize()
-        _lib.check(e.lib.zmi_graph_destroy(g.value))
-        kind = "greedy: one workgroup per slot" if e._greedy_step(0, 1) else "per-codebook workgroups"
+        us, kind = _sampler_us(e, reps)
         out[f"sampler (CFG + penalty + argmax + FSM + next embedding; {kind})"] = dict(
-            us=round(st.elapsed_time(en) * 1000.0 / n_s, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
+            us=round(us, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
     e.check_errors()
     e.release(0)
     return {"pos": pos, "kernels": out}
@@ -265,44 +228,6 @@ def _sampler_us(e, reps: int) -> tuple[float, str]:
     _lib.check(e.lib.zmi_graph_destroy(g.value))
     kind = "greedy: one workgroup per slot" if e._greedy_step(0, 1) else "per-codebook workgroups"
     return st.elapsed_time(en) * 1000.0 / n_s, kind
-
-
-def _engine_kernel_table(e, plan, pos: int, reps: int) -> dict:
-    """kernel_table for the engine plan: layer 0's QKV GEMV, the 25 layer-engine launches that end with the next
-    layer's QKV, the last one (norm_f + heads), the sampler; each layer's granules zeroed before a pass."""
-    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    out = {}
-    qkv0 = [it for kd, it in plan if kd == "gemv"]
-    eng = [it for kd, it in plan if kd == "layereng"]
-    kinds = {"qkv layer 0 (gemv: LN + QKV + RoPE + KV write)": (lambda it: e._run_gemv(it), qkv0,
-                                                                  (e.H + 2 * e.Hkv) * e.hd * e.d * 2),
-             "layer_engine<0> (attention + out_proj + fc1 + fc2 + next LN/QKV)":
-                 (lambda it: _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 0],
-                  engine_bytes(e, pos, 0)),
-             "layer_engine<1> (attention + out_proj + fc1 + fc2 + norm_f + heads)":
-                 (lambda it: _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr)), [it for it in eng if it.next == 1],
-                  engine_bytes(e, pos, 1))}
-    with torch.cuda.stream(e.stream):
-        for name, (run, items, nbytes) in kinds.items():
-            tot = 0.0
-            for r in range(reps + 1):
-                e.lay_gran.zero_()
-                st.record(e.stream)
-                for it in items:
-                    run(it)
-                en.record(e.stream)
-                en.synchronize()
-                if r:
-                    tot += st.elapsed_time(en) * 1000.0
-            us = tot / (reps * len(items))
-            out[name] = dict(us=round(us, 2), bytes=nbytes, GBps=round(nbytes / us / 1e3, 1),
-                             hbm_frac=round(nbytes / us / 1e3 / HBM_PEAK_GBS, 3), launches_per_step=len(items))
-        us, kind = _sampler_us(e, reps)
-        out[f"sampler (CFG + penalty + argmax + FSM + next embedding; {kind})"] = dict(
-            us=round(us, 2), bytes=2 * 9 * 1026 * 4, launches_per_step=1)
-    e.check_errors()
-    e.release(0)
-    return {"pos": pos, "form": "engine", "kernels": out}
 
 
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense fp16/bf16 MFMA
@@ -590,7 +515,7 @@ def c3_job(n_utt: int = 512) -> tuple[list[int], list[int]]:
     return lcs, n_new
 
 
-def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) -> dict:
+def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64, cdev=None) -> dict:
     """C3 batch-sharded throughput (north_star): the first per_gpu x world of
     the 512 C3 utterances (all 512 at 8 GPUs; per-GPU work fixed as the rank count grows), LPT-sharded
     over the ranks with no communication (shard.generate_sharded: 64 continuous-batching slots per GPU),
@@ -624,7 +549,7 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
         # a failure here is fatal: a rank that raises leaves the others inside a collective, so the run ends and
         # torch.distributed.run reports it, rather than the ranks meeting at a barrier that never completes
         from zonos_vibes_amd.shard import gather_codes
-        gathered = gather_codes(local, mine, n_utt, 0, None, dev)
+        gathered = gather_codes(local, mine, n_utt, 0, None, cdev or dev)
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -632,7 +557,7 @@ def time_c3_sharded(model, dev, rank: int, world: int, dist, per_gpu: int = 64) 
     assert mine == mine_plan
     frames = sum(int(c.shape[-1]) for c in local)
     assert frames == sum(n_new[i] for i in mine)
-    stats = torch.tensor([wall, busy, frames], dtype=torch.float64, device=dev)
+    stats = torch.tensor([wall, busy, frames], dtype=torch.float64, device=cdev or dev)
     if dist:
         allv = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allv, stats)
@@ -837,6 +762,10 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (voice clone, 60 s, 8 slots) line in `widened`")
     ap.add_argument("--no-default-cap", action="store_true",
                     help="skip the line with the engine sized for the reference default max_new_tokens")
+    ap.add_argument("--c3-per-gpu", type=int, default=64, help="C3 utterances (and slots) per GPU in `c3_sharded`")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal of the N-rank GPU run on a one-GPU box: every rank on cuda:0, gloo collectives on "
+                         "CPU tensors (timings are not per-GPU numbers)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU / gloo rehearsal of the multi-rank harness (launcher, world check, LPT plan of the C3 "
                          "set, timing reductions, end-of-batch gather) with placeholder codes; runs no kernel")
@@ -853,15 +782,21 @@ def main():
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dry_run:
         return dry_run(args, rank, world)
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if args.rehearse_one_gpu else dev  # where the collectives' tensors live
     dist = None
     if world > 1:
         import datetime
 
         import torch.distributed as dist
         # rank 0 alone runs the widened lines; the other ranks wait at the next barrier for that long
-        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(minutes=45))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=45))
+        else:
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(minutes=45))
 
     from zonos_vibes_amd.model import Zonos
     cfg = zonos_v01_transformer()
@@ -902,10 +837,10 @@ def main():
     import hashlib
     codes_sha = hashlib.sha256(ref_codes.cpu().numpy().tobytes()).hexdigest()[:16]
     if dist:
-        t = torch.tensor([elapsed], device=dev)
+        t = torch.tensor([elapsed], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        fr = torch.tensor([frames], device=dev, dtype=torch.float64)
+        fr = torch.tensor([frames], device=cdev, dtype=torch.float64)
         dist.all_reduce(fr)
         frames = int(fr.item())
     audio_s = frames * DAC_HOP / DAC_SAMPLE_RATE
@@ -917,7 +852,7 @@ def main():
     if dist:
         from zonos_vibes_amd.shard import gather_codes
         g0 = time.perf_counter()  # fatal on failure (see time_c3_sharded)
-        got = gather_codes([codes], [rank], world, device=dev)
+        got = gather_codes([codes], [rank], world, device=cdev)
         torch.cuda.synchronize()
         gather = {"ok": True, "ms": round((time.perf_counter() - g0) * 1e3, 2)}
         if rank == 0:
@@ -939,7 +874,7 @@ def main():
     dac_tf = DAC_FLOP_PER_FRAME * n_new / (breakdown["dac_decode_ms"] * 1e-3) / 1e12
     c3 = None
     if not args.no_batch:
-        c3 = time_c3_sharded(model, dev, rank, world, dist)  # last: grows the engine to 64 slots
+        c3 = time_c3_sharded(model, dev, rank, world, dist, per_gpu=args.c3_per_gpu, cdev=cdev)  # last: grows the engine
     out = None
     if rank == 0:
         out = {

@@ -378,18 +378,9 @@ int zmi_version(void);
  *   workgroup, activation tiles DMA'd two ahead, one barrier per tile) where it measured faster than the
  *   32-column tile loop; 0 = always the tile loop; bit 1: the dense-pair MFMA forms of the many-row form and of
  *   zmi_gemv_splitk (16 real columns per MFMA instead of 8, same bits; 1 = the M8 forms).
- *   ZMI_OPT_AF_DEPTH (default 3): weight loads each streaming wave of zmi_attn_ffn_block keeps in flight (1 KiB
- *          each; 2, 3, 4, 6 or 0 = unthrottled): the launch's latency-bound hand-offs queue behind whatever the
- *          chip has in flight, so the weight stream is issued progressively.
- *   ZMI_OPT_ENG_FLY (default 8): weight-ring slots (8 KiB) zmi_layer_engine's loader wave keeps in flight (1..8);
- *   ZMI_OPT_ENG_THIN (default 2): the same while a service wave of the CU polls a hand-off (1..ENG_FLY).
- *   ZMI_OPT_ENG_HOLD (default 1): zmi_layer_engine's attention-chunk workgroups issue no weights until their K / V
- *          landed.
- *   ZMI_OPT_ENG_PF (default 1): zmi_layer_engine's prefetch wave warms the Infinity Cache with the workgroup's
- *          later weight slots during the attention phase.
- *   ZMI_OPT_ENG_DELAY (default 0): ns the non-attention workgroups' weight loaders wait at launch start.
- *   ZMI_OPT_ENG_START (default 1): how zmi_ffn_engine's rings start: 0 = every slot at once, 1 = the out_proj slot
- *          first and landed before the fc1 slots are issued, 2 = the out_proj slot and one fc1 slot, then the rest.
+ *   ZMI_OPT_GEMV_SPREAD > 1: at most that many single-tile GEMV workgroups per CU (an occupancy probe).
+ *   Options 2..9: reserved (knobs of the fused / persistent decode forms measured slower and removed in round 6;
+ *          their sources are on the git branch diag-forms).
  *   ZMI_OPT_DAC_WIDE (default 1): DAC convs on 256-row time tiles (512-thread workgroups) when the output has at
  *          least ZMI_OPT_DAC_WIDE_MIN (default 256) 256-row x 32-channel units; 0 = always 128-row tiles, 2 = always
  *          256.
@@ -409,8 +400,7 @@ int zmi_version(void);
  *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group.
  *   ZMI_OPT_SPLITK_STAGE (default 1): zmi_gemv_splitk stages 2 (K segment 1024) or 4 (512) 16-row tiles per LDS
  *          buffer, so twice the activation bytes are in flight per CU (~132 KB of LDS); 0 = one tile per buffer. */
-enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_AF_DEPTH = 2, ZMI_OPT_AF_DELAY = 3, ZMI_OPT_ENG_START = 4,
-       ZMI_OPT_ENG_FLY = 5, ZMI_OPT_ENG_THIN = 6, ZMI_OPT_ENG_HOLD = 7, ZMI_OPT_ENG_PF = 8, ZMI_OPT_ENG_DELAY = 9,
+enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, /* 2..9 reserved */
        ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
        ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_SPLITK_WGS = 16, ZMI_OPT_SPLITK_STAGE = 17,
        ZMI_OPT_COUNT = 18 };

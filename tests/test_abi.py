@@ -4,13 +4,11 @@ import re
 import subprocess
 
 import numpy as np
-import pytest
 from zonos_vibes_amd import _lib
 from zonos_vibes_amd import synthetic as syn
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "zonos_hip.h")
-DIAG_HEADER = os.path.join(REPO, "include", "zonos_diag.h")
 
 
 def declared_symbols(header=HEADER):
@@ -21,19 +19,12 @@ def declared_symbols(header=HEADER):
 
 def test_header_matches_binding_table():
     assert declared_symbols() == _lib.EXPORTED
-    assert declared_symbols(DIAG_HEADER) == _lib.DIAG_EXPORTED
 
 
-def test_product_library_holds_no_diagnostic_form():
-    """The measured-slower decode forms live in libzonos_diag.so only (zonos_diag.h)."""
+def test_library_exports_only_declared_symbols():
+    """Every exported zmi_ symbol is declared in the header (no undeclared or leftover diagnostic entry points)."""
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
-    assert not set(re.findall(r"\s[TW]\s+(zmi_\w+)", out)) & set(_lib.DIAG_EXPORTED)
-
-
-@pytest.mark.skipif(not _lib.diag_available(), reason="libzonos_diag.so not built (`build --diag`)")
-def test_diag_library_exports_its_symbols():
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.DIAG_PATH], capture_output=True, text=True).stdout
-    assert set(_lib.DIAG_EXPORTED) <= set(re.findall(r"\s[TW]\s+(zmi_\w+)", out))
+    assert set(re.findall(r"\s[TW]\s+(zmi_\w+)", out)) <= set(declared_symbols())
 
 
 def test_library_exports_every_declared_symbol():

@@ -181,12 +181,7 @@ def test_full_depth_per_layer_error(full):
         e.delayed[0, :, : delayed.shape[-1]] = delayed.to(DEV, torch.int32)
         e.refresh_inputs()
     e.stream.synchronize()
-    ffn = e.ffn_block
-    e.ffn_block = False  # launch by launch: out_proj and fc1 as their own GEMVs (the fused launch gives the same bits)
-    e._build_plan()
-    plan = e._plan(2, "none")
-    e.ffn_block = ffn
-    e._build_plan()
+    plan = e._plan(2, "none")  # launch by launch: QKV, attention, out_proj, fc1, fc2 as their own launches
     layer_out, mixer, mlp = [], {}, {}
     scratch = torch.zeros(2, e.d, dtype=torch.bfloat16, device=DEV)
     res_i = 0

@@ -1,6 +1,6 @@
 """The bench's C5 share (8 voice-clone utterances of 60 s after a 430-frame prefix) on its own.
 
-    python tools/bench_c5.py [n_new] [JSON engine options, e.g. '{"ffn_block": false}'] [slots]
+    python tools/bench_c5.py [n_new] [JSON engine options, e.g. '{"attn_prefetch_blocks": 128}'] [slots]
 """
 import json
 import os

@@ -32,7 +32,6 @@ def main():
                         max_slots=args.slots)
     e = m.engine
     e.attn_block = False
-    e.ffn_block = False
     rows = 2 * args.slots
     with torch.cuda.stream(e.stream):
         e.row_pos[:rows] = args.pos

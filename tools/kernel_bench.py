@@ -45,7 +45,6 @@ def main():
         e.vc.normal_()
     e.stream.synchronize()
     e.attn_block = False  # the per-kernel breakdown of the unfused plan first
-    e.ffn_block = False
     plan = e._plan(rows)
     kinds = {"qkv": _lib.EPI_QKV, "swiglu(fc1)": _lib.EPI_SWIGLU, "logits(heads)": _lib.EPI_LOGITS}
     groups = {k: [it for kd, it in plan if kd == "gemv" and it[1] == epi] for k, epi in kinds.items()}

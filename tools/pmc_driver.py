@@ -5,13 +5,11 @@ C2 mean position, on the synthetic Zonos-v0.1 engine (B = 1, two CFG rows).
     rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fc1 -o pmc -- \
         python tools/pmc_driver.py fc1
     rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attn        (and WRITE_SIZE)
-    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention)
-    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py ffnblk      (fused out_proj + fc1)
-    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py engine      (zmi_layer_engine, layers 0..24)
+    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py attnblk     (fused QKV + attention + out_proj)
+    rocprofv3 --pmc FETCH_SIZE ... -- python tools/pmc_driver.py fc2         (the fc2 GEMV)
     rocprofv3 --pmc SQ_LDS_BANK_CONFLICT ... -- python tools/pmc_driver.py step   (the whole default decode step)
 then tools/pmc_summary.py turns the counter CSV into the per-launch JSON kept under profiles/.
 """
-import ctypes
 import os
 import sys
 
@@ -38,29 +36,16 @@ def main(which: str, reps: int = 2):
         e.vc.normal_()
     e.stream.synchronize()
     e.pos_hi[0] = POS
-    if which == "fc1":  # the fc1 GEMV as the C2 step runs it (its own launch)
-        e.ffn_block = False
-        e._build_plan()
-    if which == "ffnblk":  # the fused out_proj + fc1 launch (off by default)
-        e.ffn_block = True
-        e._build_plan()
-    if which not in ("engine", "step"):
-        e.layer_engine = False  # the launch plan's kernels
-        e._build_plan()
     plan = e._plan(2, e._segments(1, 1)[0][1])  # the form the decode step uses at POS
     for _ in range(reps):
-        if which == "fc1":
+        if which in ("fc1", "fc2"):
             for kind, it in plan:
-                if kind == "gemv" and it[1] == _lib.EPI_SWIGLU:
+                if kind == "gemv" and ((it[1] == _lib.EPI_SWIGLU) if which == "fc1" else
+                                       (it[1] == _lib.EPI_RESIDUAL and it[0].K == e.F)):
                     e._run_gemv(it)
         elif which == "attn":
             for i in range(e.L):
                 e._attention(i, e.q, 2, None, e.row_pos, e.smax - 1, e.attn)
-        elif which == "ffnblk":  # the fused out_proj + fc1 launch of every layer (granules fresh per launch)
-            for kind, it in plan:
-                if kind == "ffnblk":
-                    e.ffn_gran[it[2]].zero_()
-                    e._run_ffn_block(it)
         elif which == "attnblk":  # the fused QKV + attention launch of every layer (granules fresh per rep)
             e.blk_gran.zero_()
             for kind, it in plan:
@@ -68,11 +53,6 @@ def main(which: str, reps: int = 2):
                     e._run_attn_block(it)
         elif which == "step":  # the whole C2 decode step (launch plan + sampler) at POS, position held
             e.enqueue_step(form=e._segments(1, 1)[0][1])
-        elif which == "engine":  # the layer engine launches with the next layer's QKV (granules fresh per rep)
-            e.lay_gran.zero_()
-            for kind, it in plan:
-                if kind == "layereng" and it.next == 0:
-                    _lib.check(e.dlib.zmi_layer_engine(ctypes.byref(it), e.sptr), "layer_engine")
         else:
             raise SystemExit(f"unknown driver {which}")
     e.stream.synchronize()

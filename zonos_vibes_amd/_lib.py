@@ -19,14 +19,7 @@ c_int_p = ctypes.POINTER(ctypes.c_int)
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
 OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
 OPT_GEMM_ROWS = 1
-OPT_AF_DEPTH = 2
-OPT_AF_DELAY = 3
-OPT_ENG_START = 4
-OPT_ENG_FLY = 5
-OPT_ENG_THIN = 6
-OPT_ENG_HOLD = 7
-OPT_ENG_PF = 8
-OPT_ENG_DELAY = 9
+# 2..9: reserved (the removed diagnostic forms' knobs)
 OPT_DAC_WIDE = 10
 OPT_DAC_WIDE_MIN = 11
 OPT_ATTNBLK_SPREAD = 12
@@ -58,26 +51,6 @@ class GemvArgs(ctypes.Structure):
 class Prefetch(ctypes.Structure):
     _fields_ = [("ptr", c_void_p * 2), ("bytes", c_int64 * 2), ("sink", c_void_p), ("blocks", c_int),
                 ("reserved", c_int)]
-
-
-class FfnEngineArgs(ctypes.Structure):
-    _fields_ = [
-        ("w_out", c_void_p), ("w_fc1", c_void_p), ("w_fc2", c_void_p), ("ln_w", c_void_p), ("ln_b", c_void_p),
-        ("eps", c_float), ("M", c_int), ("attn", c_void_p), ("x", c_void_p), ("h", c_void_p),
-        ("ld_attn", c_int), ("ldx", c_int), ("ldh", c_int), ("reserved", c_int),
-        ("row_pos", c_void_p), ("gran", c_void_p), ("err", c_void_p), ("diag", c_void_p),
-    ]
-
-
-class LayerEngineArgs(ctypes.Structure):
-    _fields_ = [
-        ("w_out", c_void_p), ("w_fc1", c_void_p), ("w_fc2", c_void_p), ("w_next", c_void_p),
-        ("ln2_w", c_void_p), ("ln2_b", c_void_p), ("lnn_w", c_void_p), ("lnn_b", c_void_p),
-        ("eps", c_float), ("M", c_int), ("smax", c_int), ("next", c_int),
-        ("row_pos", c_void_p), ("x", c_void_p), ("q", c_void_p), ("k_cache", c_void_p), ("v_cache", c_void_p),
-        ("k_next", c_void_p), ("v_next", c_void_p), ("rope", c_void_p), ("attn_out", c_void_p), ("logits", c_void_p),
-        ("gran", c_void_p), ("err", c_void_p), ("diag", c_void_p),
-    ]
 
 
 class Sampling(ctypes.Structure):
@@ -193,26 +166,8 @@ _SIGS = {
     "zmi_get_option": (c_int, [c_int]),
 }
 
-# libzonos_diag.so (include/zonos_diag.h): measured-slower decode forms, built by `build --diag`
-_DIAG_SIGS = {
-    "zmi_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), c_void_p, c_void_p, c_void_p]),
-    "zmi_ffn_block_gran_words": (c_int64, [c_int]),
-    "zmi_ffn_engine": (c_int, [ctypes.POINTER(FfnEngineArgs), c_void_p]),
-    "zmi_ffn_engine_gran_words": (c_int64, [c_int]),
-    "zmi_layer_engine": (c_int, [ctypes.POINTER(LayerEngineArgs), c_void_p]),
-    "zmi_layer_engine_gran_words": (c_int64, [c_int]),
-    "zmi_layer_engine_max_pos": (c_int, []),
-    "zmi_attn_ffn_block": (c_int, [ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs), ctypes.POINTER(GemvArgs),
-                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
-    "zmi_attn_ffn_gran_words": (c_int64, [c_int]),
-    "zmi_attn_ffn_max_pos": (c_int, []),
-}
-
 EXPORTED = sorted(_SIGS)
-DIAG_EXPORTED = sorted(_DIAG_SIGS)
-DIAG_PATH = os.path.join(HERE, "libzonos_diag.so")
 _lib = None
-_diag = None
 ABI_VERSION = 4  # zmi_version() of the library this binding (and its weight packers) is written for
 
 
@@ -237,27 +192,6 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         _lib = load()
     return _lib
-
-
-def diag_available() -> bool:
-    return os.path.exists(DIAG_PATH)
-
-
-def diag() -> ctypes.CDLL:
-    """The diagnostic library (zonos_diag.h). It is not part of the product path: nothing on by default calls it."""
-    global _diag
-    if _diag is None:
-        lib()  # libzonos_hip.so first: the diagnostic library resolves its error / option state there
-        if not diag_available():
-            raise RuntimeError(f"{DIAG_PATH} is missing: these decode forms are diagnostics, built only by "
-                               "`python -m zonos_vibes_amd.build --diag`")
-        d = ctypes.CDLL(DIAG_PATH)
-        for name, (res, args) in _DIAG_SIGS.items():
-            fn = getattr(d, name)
-            fn.restype = res
-            fn.argtypes = args
-        _diag = d
-    return _diag
 
 
 def check(rc: int, what: str = "") -> None:

@@ -1,9 +1,6 @@
 """Build libzonos_hip.so in-tree with hipcc for gfx950 (no JIT cache, travels with the repo).
 
-    python -m zonos_vibes_amd.build [--force] [--diag]
-
---diag also builds libzonos_diag.so (include/zonos_diag.h): the fused / persistent decode forms measured slower
-than the product plan, kept for their tests and timing tools, linked against libzonos_hip.so.
+    python -m zonos_vibes_amd.build [--force]
 """
 from __future__ import annotations
 
@@ -16,14 +13,12 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(HERE, "libzonos_hip.so")
-DIAG_LIB = os.path.join(HERE, "libzonos_diag.so")
 SOURCES = ["zmi_gemv.hip"] + [f"zmi_gemv_e{i}.hip" for i in range(6)] + ["zmi_attn.hip", "zmi_attnblk.hip", "zmi_sample.hip",
                                                                         "zmi_dac.hip", "zmi_misc.hip", "zmi_cond.hip",
                                                                         "zmi_mamba.hip", "zmi_mambablk.hip",
                                                                         "zmi_gemm_splitk.hip"]
-DIAG_SOURCES = ["zmi_ffnblk.hip", "zmi_attnffn.hip", "zmi_engine.hip", "zmi_layer.hip"]
 HEADERS = ["zmi_common.h", "zmi_kernels.h", "zmi_gemv_impl.h", "zmi_attn_merge.h", "zmi_attn_ds.h", "zmi_mamba_step.h",
-           "zmi_prefetch.h", "zmi_engine.h"]
+           "zmi_prefetch.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-result",
          f"-I{INCLUDE}", f"-I{CSRC}"]
@@ -36,19 +31,15 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8, diag: bool = False) -> str:
-    lib = _build(SOURCES, LIB, [], force, verbose, jobs)
-    if diag:
-        # resolves zmi_fail_msg / zmi_option / zmi_cu_count from libzonos_hip.so next to it
-        _build(DIAG_SOURCES, DIAG_LIB, [f"-L{HERE}", "-lzonos_hip", "-Wl,-rpath,$ORIGIN"], force, verbose, jobs)
-    return lib
+def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
+    return _build(SOURCES, LIB, [], force, verbose, jobs)
 
 
 def _build(sources: list[str], lib: str, link: list[str], force: bool, verbose: bool, jobs: int) -> str:
     objdir = os.path.join(HERE, "build")
     flags = FLAGS
     os.makedirs(objdir, exist_ok=True)
-    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, h) for h in ("zonos_hip.h", "zonos_diag.h")]
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "zonos_hip.h")]
     objs, procs = [], []
     for src in sources:
         sp = os.path.join(CSRC, src)
@@ -84,4 +75,4 @@ def _wait(item):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, diag="--diag" in sys.argv)
+    build(force="--force" in sys.argv)

@@ -95,18 +95,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
     // M_j is formed while V^T is in flight (one memory round trip, not two)
     const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
     const int p0 = min(key0 + wave * 32 + 8 * h4, (last_key & ~7));
-#ifdef ZMI_ATTN_LATE
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-      vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
-#endif
     const float mine = t < dep * G ? lu[2 * t + 1] : -INFINITY;  // e = t = chunk * G + head
     const float4 sv = t * 4 < G * CH ? ld4(po + t * 4) : float4{0.f, 0.f, 0.f, 0.f};
-#ifndef ZMI_ATTN_LATE
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
       vf[dt] = *reinterpret_cast<const uint4*>(a.v + kvbase + (size_t)(16 * dt + c16) * a.smax + p0);
-#endif
     float m = mine;
     for (int e = t + NT; e < dep * G; e += NT) m = fmaxf(m, lu[2 * e + 1]);  // positions >= 64 NT / G only
     if (t * 4 < G * CH) *reinterpret_cast<float4*>(&sc[(t * 4) / CH][(t * 4) % CH]) = sv;
@@ -330,11 +323,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G == 4 ? 6 :
   __syncthreads();
   const float* ou = a.part_o + (size_t)unit * a.nch * G * HD;
   const float* lu = a.part_lm + (size_t)unit * a.nch * G * 2;
-#ifdef ZMI_ATTN_M4
-  if constexpr (false) {
-#else
   if constexpr (MODE == 2) {  // 2 dims per thread, 16 chunks' loads in flight
-#endif
     for (int e = t * 2; e < G * HD; e += NT * 2) {
       const int g = e / HD, d = e - g * HD;
       const float2 r = merge2<16>(ou, lu, nc, g, d, G);

@@ -146,35 +146,10 @@ class HipEngine:
         # ... also in the 24-chunk form (batch-1 steps at positions 1024 .. 3071)
         self.attn_oproj_wide = True
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
-        # out_proj + fc1 as ONE launch (zmi_ffn_block) for <= `ffn_block_rows` rows at the v0.1 dims on a 256-CU
-        # device: fc1's weights stream while the out_proj chain runs (identical bits). Off: it loses to the
-        # separate launches at every row count measured (C2 step 972 us without it against 983 with it,
-        # profiles/r03_ffnblk_c2_ab.jsonl; C5-shaped steps at 4 / 8 / 16 rows 1.21 / 1.52 / 2.06 ms against
-        # 1.26 / 1.61 / 2.27, profiles/r03_ffnblk_rows_ab.jsonl: every workgroup DMAs all rows and gathers all
-        # rows' residual granules, and the separate out_proj finds its weights prefetched by the attention block)
-        self.ffn_block = False
-        self.ffn_block_rows = 2
-        # attention + out_proj + fc1 as ONE launch after a plain QKV launch (zmi_attn_ffn_block) for <= 2 rows
-        # (batch 1) at positions < 1024: out_proj's and fc1's weights stream under the attention chain
-        # (identical bits). Off: measured slower (C2 step 1042-1075 us against 984, tools/step_ab.py; every
-        # hand-off of the chain takes 3-5 us under the weight stream against ~1.5 on an idle memory system,
-        # DESIGN.md §5)
-        self.attn_ffn = False
         # fc2 (K = 8192) over >= `splitk_rows` rows and out_proj (K = 2048) over >= `splitk_o_rows` rows as
         # split-K GEMMs (zmi_gemv_splitk: each column block reads the activation rows once, and the reduce can
         # write the next LayerNorm; identical bits); 0 = never. out_proj split-K: C5-shaped 16-row step 1.732 vs
         # 1.741 ms, C3 sample 151.3 vs 149.5x (profiles/r03_splitk_oproj2_ab.jsonl)
-        # out_proj + norm2 + fc1 + fc2 as ONE persistent launch (zmi_ffn_engine: 256 workgroups, one per CU, LDS-DMA
-        # weight rings running ahead of the in-launch hand-offs) for <= 2 rows at the v0.1 dims; identical bits.
-        # Off: 28.2 us per layer against 25.5 for the three launches (tools/ffn_engine_bench.py)
-        self.ffn_engine = False
-        # the whole decode layer as ONE persistent launch (zmi_layer_engine: attention, out_proj, fc1, fc2 and the
-        # next layer's QKV / the heads, 256 workgroups, LDS-DMA weight rings) for <= 2 rows at the v0.1 dims and
-        # positions <= zmi_layer_engine_max_pos(); identical bits (the "engine" form). Off: the C2 step takes
-        # 1138-1167 us with it against 1011-1018 us with the launch plan on the same box (tools/step_ab.py,
-        # profiles/r04_engine_*): each in-launch all-gather costs ~3 us against ~1.5 us for a kernel boundary
-        # 
-        self.layer_engine = False
         self.splitk_rows = 16
         self.splitk_o_rows = 16
         # the hybrid's Mamba2 out_proj (K = d_ssm = 4096, EPI_STORE) over >= `splitk_m_rows` rows (its prefill: the
@@ -198,24 +173,6 @@ class HipEngine:
         self.pos_hi = [0] * self.S
         self.n_kv = self._kv_layers()
         self._alloc()
-
-    @property
-    def dlib(self):
-        """libzonos_diag.so: the fused / persistent decode forms measured slower than this plan (ffn_block,
-        attn_ffn, ffn_engine, layer_engine; all off by default). Loaded on first use; never on the product path."""
-        return _lib.diag()
-
-    def _diag_alloc(self):
-        """Hand-off granule areas of the diagnostic forms, zeroed (as a new utterance needs them)."""
-        if self.eng_gran is not None:
-            return
-        z = lambda *shape: torch.zeros(*shape, dtype=torch.int64, device=self.dev)  # noqa: E731
-        with torch.cuda.stream(self.stream):
-            one = self.S == 1 and not self.hybrid
-            self.eng_gran = z(self.L if one else 0, max(self.dlib.zmi_ffn_engine_gran_words(2), 0))
-            self.lay_gran = z(self.L if one else 0, max(self.dlib.zmi_layer_engine_gran_words(2), 0))
-            self.ffn_gran = z(self.L, self.R, self.dlib.zmi_ffn_block_gran_words(1))
-            self.attn_gran = z(self.L, self.R, self.dlib.zmi_attn_ffn_gran_words(1))
 
     def _kv_layers(self) -> int:
         """Layers with a KV cache (every layer of the transformer)."""
@@ -250,10 +207,7 @@ class HipEngine:
             self.blk_rows = min(R, BLK_ROWS_MAX)
             self.blk_gran = z(self.n_kv, self.blk_rows, self.lib.zmi_attn_block_gran_words(1, self.Hkv),
                               dt=torch.int64)
-            self.blk_err = z(8, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink, [3] ffn_block,
-            # [4] attn_ffn_block, [5] ffn_engine, [6] layer_engine
-            # hand-off granules of the diagnostic forms (zonos_diag.h), allocated on first use (_diag_alloc)
-            self.eng_gran = self.lay_gran = self.ffn_gran = self.attn_gran = None
+            self.blk_err = z(4, dt=torch.int32)  # [0] attn_block, [1] mamba_block, [2] prefetch sink
             # zmi_gemv_splitk's fp32 segment sums (fc2 / out_proj over many rows: decode and prefill)
             self.splitk_part = z(self.lib.zmi_gemv_splitk_floats(max(R, self.pre_rows), d), dt=torch.float32)
             self.samp_cnt = z(S, dt=torch.int32)
@@ -378,63 +332,10 @@ class HipEngine:
             return 24 | _lib.ATTNBLK_SPLIT
         return self.attn_self_slices | _lib.ATTNBLK_SELF if form == "self" else self.attn_block_slices
 
-    def _use_ffn_block(self, rows: int) -> bool:
-        return (self.ffn_block and rows <= self.ffn_block_rows and self.d == 2048 and self.F == 8192 and self.H * self.hd == 2048
-                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
-
-    def _use_ffn_engine(self, rows: int) -> bool:
-        return (self.ffn_engine and rows <= 2 and self.S == 1 and self.d == 2048 and self.F == 8192
-                and self.H * self.hd == 2048 and not self.hybrid
-                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
-
-    def _use_layer_engine(self, rows: int) -> bool:
-        return (self.layer_engine and rows <= 2 and self.S == 1 and self.d == 2048 and self.F == 8192
-                and self.H == 16 and self.Hkv == 4 and self.hd == 128 and not self.hybrid
-                and torch.cuda.get_device_properties(self.dev).multi_processor_count >= 256)
-
-    def _layer_engine_args(self, i: int, rows: int) -> _lib.LayerEngineArgs:
-        self._diag_alloc()
-        w, L = self.w, self.L
-        lw, last = w["layers"][i], i + 1 == L
-        e = _lib.LayerEngineArgs()
-        e.w_out, e.w_fc1, e.w_fc2 = lw["out"].data_ptr(), lw["fc1"].data_ptr(), lw["fc2"].data_ptr()
-        e.ln2_w, e.ln2_b = lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr()
-        if last:
-            e.w_next, e.lnn_w, e.lnn_b, e.next = w["heads"].data_ptr(), w["nf_w"].data_ptr(), w["nf_b"].data_ptr(), 1
-            e.logits = self.logits.data_ptr()
-        else:
-            nw = w["layers"][i + 1]
-            e.w_next, e.lnn_w, e.lnn_b, e.next = nw["qkv"].data_ptr(), nw["ln1_w"].data_ptr(), nw["ln1_b"].data_ptr(), 0
-            e.k_next, e.v_next, e.rope = self.kc[i + 1].data_ptr(), self.vc[i + 1].data_ptr(), self.rope.data_ptr()
-        e.eps, e.M, e.smax = self.eps, rows, self.smax
-        e.row_pos, e.x, e.q = self.row_pos.data_ptr(), self.x.data_ptr(), self.q.data_ptr()
-        e.k_cache, e.v_cache = self.kc[i].data_ptr(), self.vc[i].data_ptr()
-        e.attn_out = None
-        e.gran, e.err = self.lay_gran[i].data_ptr(), self.blk_err[6:].data_ptr()
-        return e
-
-    def _ffn_engine_args(self, lw, i: int, rows: int) -> _lib.FfnEngineArgs:
-        self._diag_alloc()
-        e = _lib.FfnEngineArgs()
-        e.w_out, e.w_fc1, e.w_fc2 = lw["out"].data_ptr(), lw["fc1"].data_ptr(), lw["fc2"].data_ptr()
-        e.ln_w, e.ln_b, e.eps = lw["ln2_w"].data_ptr(), lw["ln2_b"].data_ptr(), self.eps
-        e.M = rows
-        e.attn, e.ld_attn = self.attn.data_ptr(), self.H * self.hd
-        e.x, e.ldx = self.x.data_ptr(), self.d
-        e.h, e.ldh = None, 0
-        e.row_pos, e.gran, e.err = self.row_pos.data_ptr(), self.eng_gran[i].data_ptr(), self.blk_err[5:].data_ptr()
-        return e
-
-    def _use_attn_ffn(self, rows: int, form: str) -> bool:
-        return (self.attn_ffn and form == "split" and rows * self.Hkv <= 8 and rows <= 4 and self._use_ffn_block(rows)
-                and self.H == 4 * self.Hkv and self.hd == 128)
-
     def _forms(self, rows: int) -> list:
         """(form, last position it accepts) of the fused decode block, fastest first; "none" = separate
         QKV and attention launches (any position)."""
         out = []
-        if self._use_layer_engine(rows):
-            out.append(("engine", self.dlib.zmi_layer_engine_max_pos()))
         if (self.attn_block and rows <= min(self.attn_block_rows, self.blk_rows) and self.d == 2048
                 and self.H == 4 * self.Hkv):
             for f in self.attn_forms:
@@ -468,16 +369,6 @@ class HipEngine:
         """Decode-step launches for the first `rows` rows (slots 0 .. rows/2 - 1). Every kernel's
         per-row arithmetic is independent of `rows` and of the launch form, so a slot decodes
         identically in any plan."""
-        if (rows, form) not in self._plans and form == "engine":
-            # layer 0's QKV (LayerNorm prologue, RoPE, KV write), then one persistent launch per layer, the last
-            # of which also runs norm_f + the heads
-            lw0, d, qd = self.w["layers"][0], self.d, self.H * self.hd
-            qkv_n = (self.H + 2 * self.Hkv) * self.hd
-            plan = [("gemv", self._gemv(lw0["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                        ln=(lw0["ln1_w"], lw0["ln1_b"]), kv=(self.kc[0], self.vc[0]),
-                                        row_kv=self.row_kv, row_pos=self.row_pos))]
-            plan += [("layereng", self._layer_engine_args(i, rows)) for i in range(self.L)]
-            self._plans[(rows, form)] = plan
         if (rows, form) not in self._plans:
             w, d, qd = self.w, self.d, self.H * self.hd
             qkv_n = (self.H + 2 * self.Hkv) * self.hd
@@ -503,20 +394,6 @@ class HipEngine:
 
             for i, lw in enumerate(w["layers"]):
                 kv = (self.kc[i], self.vc[i])
-                if self._use_attn_ffn(rows, form):
-                    # QKV launch, then attention + out_proj + fc1 in one launch, then fc2
-                    qkv = self._gemv(lw["qkv"], self.x, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
-                                     ln=(lw["ln1_w"], lw["ln1_b"]), kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
-                    plan.append(("gemv", qkv))
-                    o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
-                    o_item[0].row_pos = self.row_pos.data_ptr()
-                    f_item = self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
-                                        ln=(lw["ln2_w"], lw["ln2_b"]))
-                    qa = _lib.GemvArgs.from_buffer_copy(qkv[0])
-                    qa.row_kv = None  # decode: query row r caches into KV row r (one dependent load fewer)
-                    plan.append(("attnffn", (qa, o_item[0], f_item[0], i)))
-                    plan.append(("gemv", self._gemv(lw["fc2"], self.h, rows, d, self.F, _lib.EPI_RESIDUAL, self.x, d)))
-                    continue
                 xin, ln = normed((lw["ln1_w"], lw["ln1_b"])) if not fused else (self.x, (lw["ln1_w"], lw["ln1_b"]))
                 qkv = self._gemv(lw["qkv"], xin, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                  ln=ln, kv=kv, row_kv=self.row_kv, row_pos=self.row_pos)
@@ -545,19 +422,11 @@ class HipEngine:
                         apf.bytes[1] = min(lw["fc1"].numel() * 2, int(self.attn_prefetch_fc1_mb * 2 ** 20))
                         apf.sink, apf.blocks = self.blk_err[2:].data_ptr(), self.attn_prefetch_blocks
                     plan.append(("attn", (i, apf)))
-                if self._use_ffn_engine(rows):
-                    plan.append(("ffneng", self._ffn_engine_args(lw, i, rows)))
-                    continue
                 o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
                 if oproj:  # out_proj ran inside the fused block
                     xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
                     plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
                                                     self.F, ln=ln)))
-                elif self._use_ffn_block(rows):
-                    o_item[0].row_pos = self.row_pos.data_ptr()
-                    f_item = self._gemv(lw["fc1"], self.x, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F,
-                                        ln=(lw["ln2_w"], lw["ln2_b"]))
-                    plan.append(("ffnblk", (o_item[0], f_item[0], i)))
                 else:
                     if pre and self._use_splitk(*o_item) and d == 2048:
                         # the split-K reduce also writes LayerNorm(new x) for fc1 (no pre-pass launch)
@@ -609,30 +478,15 @@ class HipEngine:
         wide_ok = form == "split24" and self.attn_oproj_wide
         return self.attn_oproj and (form == "split" or wide_ok) and not self.hybrid and self.H * self.hd == self.d
 
-    def _run_attn_ffn(self, item):
-        a, o, f, i = item
-        self._diag_alloc()
-        _lib.check(self.dlib.zmi_attn_ffn_block(ctypes.byref(a), ctypes.byref(o), ctypes.byref(f),
-                                               self.blk_gran[i].data_ptr(), self.attn_gran[i].data_ptr(),
-                                               self.ffn_gran[i].data_ptr(), self.blk_err[4:].data_ptr(),
-                                               self.attn.data_ptr(), self.H * self.hd, self.sptr), "attn_ffn_block")
-
-    def _run_ffn_block(self, item):
-        o, f, i = item
-        self._diag_alloc()
-        _lib.check(self.dlib.zmi_ffn_block(ctypes.byref(o), ctypes.byref(f), self.ffn_gran[i].data_ptr(),
-                                          self.blk_err[3:].data_ptr(), self.sptr), "ffn_block")
-
     def check_errors(self):
         """Raise if a launch gave up waiting on an in-launch hand-off (bounded spin) or refused a row past
         its reach. The flags are cleared first, so a later utterance (after a fresh prefill) runs clean."""
         attn = int(self.attn_work[:4].view(torch.int32).item())
-        blk, mamba, _, ffn, af, eng, leng = (int(v) for v in self.blk_err[:7].tolist())
-        if attn or blk or mamba or ffn or af or eng or leng:
+        blk, mamba = (int(v) for v in self.blk_err[:2].tolist())
+        if attn or blk or mamba:
             with torch.cuda.stream(self.stream):  # ordered with the engine's launches
                 self.attn_work[:4].zero_()
                 self.blk_err[:2].zero_()
-                self.blk_err[3:7].zero_()
             self.stream.synchronize()
         if attn:
             raise RuntimeError("attention: a cross-block hand-off timed out (results of that launch are invalid)")
@@ -641,16 +495,6 @@ class HipEngine:
                                "(results are invalid)")
         if mamba:
             raise RuntimeError("mamba_block: a wait for the in_proj output timed out (results are invalid)")
-        if ffn:
-            raise RuntimeError("ffn_block: a wait for the new residual rows timed out (results are invalid)")
-        if af:
-            raise RuntimeError("attn_ffn_block: a hand-off wait timed out or a row was past the form's reach "
-                               "(results are invalid)")
-        if eng:
-            raise RuntimeError("ffn_engine: an in-launch hand-off wait timed out (results are invalid)")
-        if leng:
-            raise RuntimeError("layer_engine: an in-launch hand-off wait timed out or a position was past its reach "
-                               "(results are invalid)")
 
     def refresh_inputs(self):
         """Recompute every slot's input embedding + row tables from the delayed codes (after a host-side
@@ -696,14 +540,6 @@ class HipEngine:
                 self._run_gemv(item)
             elif kind == "attnblk":
                 self._run_attn_block(item)
-            elif kind == "ffnblk":
-                self._run_ffn_block(item)
-            elif kind == "attnffn":
-                self._run_attn_ffn(item)
-            elif kind == "layereng":
-                _lib.check(self.dlib.zmi_layer_engine(ctypes.byref(item), self.sptr), "layer_engine")
-            elif kind == "ffneng":
-                _lib.check(self.dlib.zmi_ffn_engine(ctypes.byref(item), self.sptr), "ffn_engine")
             elif kind == "splitkln":
                 (a, epi), ln = item
                 _lib.check(self.lib.zmi_gemv_splitk_ln(ctypes.byref(a), epi, self.splitk_part.data_ptr(),
@@ -858,12 +694,6 @@ class HipEngine:
         """Zero the in-launch hand-off granules of the slot's rows (tags are positions + 1)."""
         if 2 * slot < self.blk_rows:
             self.blk_gran[:, 2 * slot: 2 * slot + 2].zero_()
-        if self.eng_gran is not None:  # the diagnostic forms' areas, once allocated
-            self.ffn_gran[:, 2 * slot: 2 * slot + 2].zero_()
-            self.attn_gran[:, 2 * slot: 2 * slot + 2].zero_()
-            if slot == 0:
-                self.eng_gran.zero_()
-                self.lay_gran.zero_()
 
     def _prefill_logits(self, s_len: int, off: int = 0):
         """Heads of the last position of the cond / uncond prefill rows (starting at row `off`) -> logits_pre
