@@ -75,9 +75,10 @@ case "$cmd" in
   mfma) mfma "$@" || exit $? ;;
   round)
     prof bench 500 python bench.py --no-cpu-baseline --no-hybrid --no-batch --no-c5 --no-default-cap || exit $?
-    pmc FETCH_SIZE fc1 "gemv_kernel<2, 4, 8, 16, 1, 3, 1>" 67158016 fc1_fetch || exit $?
     pmc FETCH_SIZE attnblk attn_block_kernel 23396352 attnblk_fetch || exit $?   # QKV + out_proj + K/V at 591
     pmc WRITE_SIZE attnblk attn_block_kernel 23396352 attnblk_write || exit $?
+    pmc FETCH_SIZE fc1 "gemv_kernel<2, 4, 8, 16, 1, 3, 1>" 67158016 fc1_fetch || exit $?
+    pmc FETCH_SIZE fc2 "gemv_kernel<1, 8, 16, 8, 0, 1, 1>" 33554432 fc2_fetch || exit $?
     prof c5_2000 400 python tools/bench_c5.py 2000 || exit $?
     mfma 861 dac || exit $?
     ls -la $K
