@@ -592,51 +592,79 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   }
   if (PRO == PRO_GRMS) {
     // RMSNormGated (norm_before_gate=False): g = y (z sigmoid(z)), out = g rstd w; g recomputed in the
-    // apply pass (the same bits), sums of g^2 element by element as zmi_gated_rmsnorm
+    // apply pass (the same bits), sums of g^2 element by element as zmi_gated_rmsnorm. A wave takes its
+    // (row, part) tasks two at a time (the second clamped, its results dropped): two independent dependent-add
+    // chains in one straight-line body instead of one after the other (the K = 4096 out_proj has 4 waves for
+    // 2 rows x 4 parts)
     constexpr int NQ = ln_parts(K), CPQ = K / (512 * NQ);
     float* part = red;
     const int ntask = rows * NQ;
-    for (int task = wave; task < ntask; task += NWV) {
-      const int r = task / NQ, q = task - r * NQ;
-      const bf16_t* yr = xs + r * XROW + q * (K / NQ);
-      const float* zr = xg + r * GROW + q * (K / NQ);
-      float t = 0.f;
+    for (int task0 = wave; task0 < ntask; task0 += 2 * NWV) {
+      float t[2];
 #pragma unroll
-      for (int i = 0; i < CPQ; ++i) {
-        const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
-        const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
-        float gz[8];
-        load_gate(zr + (lane + 64 * i) * 8, gz);
+      for (int u = 0; u < 2; ++u) {
+        const int task = min(task0 + u * NWV, ntask - 1);
+        const int r = task / NQ, q = task - r * NQ;
+        const bf16_t* yr = xs + r * XROW + q * (K / NQ);
+        const float* zr = xg + r * GROW + q * (K / NQ);
+        t[u] = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float g = gate_elem(y, gz, e);
-          t += g * g;
+        for (int i = 0; i < CPQ; ++i) {
+          const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+          const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
+          float gz[8];
+          load_gate(zr + (lane + 64 * i) * 8, gz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float g = gate_elem(y, gz, e);
+            t[u] += g * g;
+          }
         }
       }
-      t = wave_sum(t);
-      if (lane == 0) part[task] = t;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) t[u] = wave_sum(t[u]);
+      if (lane == 0) {
+        part[task0] = t[0];
+        if (task0 + NWV < ntask) part[task0 + NWV] = t[1];
+      }
     }
     __syncthreads();
-    for (int task = wave; task < ntask; task += NWV) {
-      const int r = task / NQ, q = task - r * NQ;
-      const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part + r * NQ) / (float)K + a.eps);
-      bf16_t* yr = xs + r * XROW + q * (K / NQ);
-      const float* zr = xg + r * GROW + q * (K / NQ);
+    for (int task0 = wave; task0 < ntask; task0 += 2 * NWV) {
+      uint4 res[2][CPQ];
 #pragma unroll
-      for (int i = 0; i < CPQ; ++i) {
-        const int c = q * (K / NQ) / 8 + lane + 64 * i;
-        const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
-        const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
-        const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
-        const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
-        float gz[8];
-        load_gate(zr + (lane + 64 * i) * 8, gz);
-        uint32_t o[4];
+      for (int u = 0; u < 2; ++u) {
+        const int task = min(task0 + u * NWV, ntask - 1);
+        const int r = task / NQ, q = task - r * NQ;
+        const float rstd = 1.0f / sqrtf(ln_combine<NQ>(part + r * NQ) / (float)K + a.eps);
+        const bf16_t* yr = xs + r * XROW + q * (K / NQ);
+        const float* zr = xg + r * GROW + q * (K / NQ);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          o[j] = f2bf((gate_elem(y, gz, 2 * j) * rstd) * bf2f(uw[j])) |
-                 (f2bf((gate_elem(y, gz, 2 * j + 1) * rstd) * bf2f(uw[j] >> 16)) << 16);
-        *reinterpret_cast<uint4*>(yr + (lane + 64 * i) * 8) = uint4{o[0], o[1], o[2], o[3]};
+        for (int i = 0; i < CPQ; ++i) {
+          const int c = q * (K / NQ) / 8 + lane + 64 * i;
+          const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+          const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
+          const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
+          const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
+          float gz[8];
+          load_gate(zr + (lane + 64 * i) * 8, gz);
+          uint32_t o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            o[j] = f2bf((gate_elem(y, gz, 2 * j) * rstd) * bf2f(uw[j])) |
+                   (f2bf((gate_elem(y, gz, 2 * j + 1) * rstd) * bf2f(uw[j] >> 16)) << 16);
+          res[u][i] = uint4{o[0], o[1], o[2], o[3]};
+        }
+      }
+      // stores after both tasks' reads: the clamped duplicate task reads what the real one overwrites
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int task = task0 + u * NWV;
+        if (task < ntask) {
+          const int r = task / NQ, q = task - r * NQ;
+          bf16_t* yr = xs + r * XROW + q * (K / NQ);
+#pragma unroll
+          for (int i = 0; i < CPQ; ++i) *reinterpret_cast<uint4*>(yr + (lane + 64 * i) * 8) = res[u][i];
+        }
       }
     }
     __syncthreads();

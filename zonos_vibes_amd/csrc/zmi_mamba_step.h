@@ -45,6 +45,7 @@ struct StepPre {
   float ring[NI][MB_DC - 1];
   float w[NI][MB_DC];
   float bias[NI];
+  float dt_bias, A, D;      // the head's scalars: loaded with the rest, not after the in_proj values arrive
 };
 
 template <int NT>
@@ -56,6 +57,9 @@ __device__ __forceinline__ void step_prefetch(const ZmiMamba2Args& a, int h, int
 #pragma unroll
     for (int j = 0; j < 4; ++j) pre.sv[j] = reinterpret_cast<const uint4*>(st)[j];
   }
+  pre.dt_bias = a.dt_bias[h];
+  pre.A = a.A[h];
+  pre.D = a.D[h];
   const bf16_t* ring = reinterpret_cast<const bf16_t*>(a.conv_ring) + (size_t)kv * MB_DC * conv_dim;
   const bf16_t* cw = reinterpret_cast<const bf16_t*>(a.conv_w);
   const bf16_t* cb = reinterpret_cast<const bf16_t*>(a.conv_b);
@@ -99,8 +103,8 @@ __device__ __forceinline__ void step_core(const ZmiMamba2Args& a, int m, int h, 
     }
   }
   // (2) dt = softplus(dt + dt_bias), dA = exp(A dt)  (selective_state_update, tie_hdim)
-  const float dtv = softplus_f(bf2f(raw[RAW_DT]) + a.dt_bias[h]);
-  const float dA = expf(a.A[h] * dtv);
+  const float dtv = softplus_f(bf2f(raw[RAW_DT]) + pre.dt_bias);
+  const float dA = expf(pre.A * dtv);
   __syncthreads();
   if (t >= MB_NT) return;
   // (3) state update and readout: lane (p, quarter) owns state[p][32 quarter .. +31]
@@ -129,7 +133,7 @@ __device__ __forceinline__ void step_core(const ZmiMamba2Args& a, int m, int h, 
   for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = pre.sv[j];
   out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
   if (nq == 0) {
-    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * a.D[h]);
+    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * pre.D);
     if (a.gz) {  // RMSNormGated's gate of this channel, once (the out_proj GEMV's GRMS prologue multiplies)
       const float zz = bf2f(raw[RAW_Z + p]);
       a.gz[(size_t)m * a.ldy + h * MB_HD + p] = zz * (1.0f / (1.0f + expf(-zz)));

@@ -26,10 +26,30 @@
 namespace {
 
 using namespace zmi_mamba;
-constexpr int IG = 2, IW = 4, INL = 8, IRT = 16;  // in_proj role: the K = 2048 shape, 2 groups
+#ifndef ZMI_MB_IG
+#define ZMI_MB_IG 2
+#endif
+constexpr int IG = ZMI_MB_IG, IW = 4, INL = 8, IRT = 16;  // in_proj role: the K = 2048 shape, IG groups
 constexpr int NT = IG * IW * 64;
 constexpr int NGRAN = MB_HD / 2 + MB_DS + MB_HD / 2 + 1;  // x pairs, B / C pairs, z pairs, the dt pair
 constexpr unsigned SPIN = 1u << 20;
+
+// Diagnostic build only (-DZMI_GEMV_STAMPS, tools/hybrid_stamps.py): the step role stamps into the in_proj
+// args' diag area like the GEMV role (slot 0 start, 2 granules received, 3 raw values in LDS, 6 end).
+#ifdef ZMI_GEMV_STAMPS
+#define ZMI_MSTAMP(i)                                                                                     \
+  do {                                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+    if (threadIdx.x == 0 && ia.diag)                                                                      \
+      reinterpret_cast<unsigned long long*>(ia.diag)[((size_t)ia.reserved * 4096 + blockIdx.x) * 8 + (i)] = \
+          __builtin_amdgcn_s_memrealtime();                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                                    \
+  } while (0)
+#else
+#define ZMI_MSTAMP(i) \
+  do {                \
+  } while (0)
+#endif
 
 __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, int n_cb, int n_in,
                                                          const ZmiMamba2Args ma, uint64_t* gran, int gstride,
@@ -48,6 +68,7 @@ __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, i
   }
   const int b2 = b - n_in;
   const int m = b2 / ma.nheads, h = b2 - m * ma.nheads;
+  ZMI_MSTAMP(0);
   const int pos = ma.row_pos[m];
   if (pos < 0) return;  // inactive row: block-uniform, before any barrier
   const int kv = ma.row_kv ? ma.row_kv[m] : m;
@@ -84,6 +105,7 @@ __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, i
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    ZMI_MSTAMP(2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = lane + 64 * i;
@@ -103,7 +125,9 @@ __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, i
     }
   }
   __syncthreads();
+  ZMI_MSTAMP(3);
   step_core<NT>(ma, m, h, pos, kv, raw, pre, xs, bc);
+  ZMI_MSTAMP(6);
 }
 
 }  // namespace

@@ -220,6 +220,7 @@ class HybridEngine(HipEngine):
         def run():
             _lib.check(lib.zmi_mamba_block_pf(ctypes.byref(ia), ctypes.byref(sa), gp, ep, ctypes.byref(pf), s),
                        "mamba_block")
+        run.args = (ia, sa)  # for tools (tools/hybrid_stamps.py sets ia.diag)
         return run
 
     def _call_step(self, a):
