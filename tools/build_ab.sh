@@ -14,6 +14,6 @@ CXX="/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -ffp-contrac
 $CXX "$@" -c zonos_vibes_amd/csrc/$SRC.hip -o /tmp/ab_$name/p.o &
 $CXX "$@" -DZMI_ATTN_STAMPS -DZMI_GEMV_STAMPS -c zonos_vibes_amd/csrc/$SRC.hip -o /tmp/ab_$name/s.o &
 wait
-others=$(ls zonos_vibes_amd/build/*.o | grep -v $SRC)
+others=$(ls zonos_vibes_amd/build/*.o | grep -v "/$SRC\.o$")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others /tmp/ab_$name/p.o -o zonos_vibes_amd/ab/lib$name.so
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others /tmp/ab_$name/s.o -o zonos_vibes_amd/ab/libstamps_$name.so
