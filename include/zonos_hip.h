@@ -368,9 +368,16 @@ int zmi_graph_destroy(void* graph_exec);
 
 const char* zmi_last_error(void);
 /* ABI version, bumped whenever a weight layout or an option's meaning changes: 4 = channel-blocked DAC conv weights
- * [tap][ci / 32][co][32] (zmi_dac_conv / conv_t / conv_out) and the round-5 ZMI_OPT_GEMM_ROWS bits. Check it
- * before packing weights (zonos_vibes_amd/_lib.py refuses a library whose version differs). */
+ * [tap][ci / 32][co][32] (zmi_dac_conv / conv_t / conv_out) and the round-5 ZMI_OPT_GEMM_ROWS bits; 5 =
+ * ZMI_OPT_XC_HANDOFF and zmi_xcd_dealing. Check it before packing weights (zonos_vibes_amd/_lib.py refuses a library
+ * whose version differs). */
 int zmi_version(void);
+/* 1 if this device deals a launch's workgroups round-robin over its XCDs (blocks b and b + 8 on one XCD, 8
+ * distinct XCDs), 0 if not, negative on a launch error (zmi_last_error). Runs a probe launch and waits for it:
+ * call it outside graph capture. The fused attention block's chunk workgroups of one (row, kv head) hand their
+ * maxima and partials over through that XCD's L2 (ZMI_OPT_XC_HANDOFF 0) only where this holds; the engine calls it
+ * once and sets ZMI_OPT_XC_HANDOFF to 1 otherwise. */
+int zmi_xcd_dealing(void* stream);
 /* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
  *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the
  *   dispatcher spreads their workgroups evenly over the CUs instead of packing several onto one CU.
@@ -400,7 +407,7 @@ int zmi_version(void);
  *          has about this many workgroups (each row group re-reads its segment's weights); 0 = one row group.
  *   ZMI_OPT_SPLITK_STAGE (default 1): zmi_gemv_splitk stages 2 (K segment 1024) or 4 (512) 16-row tiles per LDS
  *          buffer, so twice the activation bytes are in flight per CU (~132 KB of LDS); 0 = one tile per buffer. */
-enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, /* 2..9 reserved */
+enum { ZMI_OPT_GEMV_SPREAD = 0, ZMI_OPT_GEMM_ROWS = 1, ZMI_OPT_XC_HANDOFF = 2, /* 3..9 reserved */
        ZMI_OPT_DAC_WIDE = 10, ZMI_OPT_DAC_WIDE_MIN = 11, ZMI_OPT_ATTNBLK_SPREAD = 12, ZMI_OPT_DAC_STAGE = 13,
        ZMI_OPT_DAC_STAGE_MIN = 14, ZMI_OPT_SCAN_PQ = 15, ZMI_OPT_SPLITK_WGS = 16, ZMI_OPT_SPLITK_STAGE = 17,
        ZMI_OPT_COUNT = 18 };

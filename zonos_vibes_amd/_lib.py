@@ -19,7 +19,8 @@ c_int_p = ctypes.POINTER(ctypes.c_int)
 EPI_STORE, EPI_RESIDUAL, EPI_QKV, EPI_SWIGLU, EPI_LOGITS, EPI_F32 = range(6)
 OPT_GEMV_SPREAD = 0  # zmi_set_option knobs
 OPT_GEMM_ROWS = 1
-# 2..9: reserved (the removed diagnostic forms' knobs)
+OPT_XC_HANDOFF = 2  # 0: chunk-split attention hand-offs through the XCD's L2; 1: write-through
+# 3..9: reserved (the removed diagnostic forms' knobs)
 OPT_DAC_WIDE = 10
 OPT_DAC_WIDE_MIN = 11
 OPT_ATTNBLK_SPREAD = 12
@@ -162,13 +163,14 @@ _SIGS = {
     "zmi_graph_destroy": (c_int, [c_void_p]),
     "zmi_last_error": (ctypes.c_char_p, []),
     "zmi_version": (c_int, []),
+    "zmi_xcd_dealing": (c_int, [c_void_p]),
     "zmi_set_option": (c_int, [c_int, c_int]),
     "zmi_get_option": (c_int, [c_int]),
 }
 
 EXPORTED = sorted(_SIGS)
 _lib = None
-ABI_VERSION = 4  # zmi_version() of the library this binding (and its weight packers) is written for
+ABI_VERSION = 5  # zmi_version() of the library this binding (and its weight packers) is written for
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:

@@ -374,6 +374,8 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const int pos = a.pos[qi];
   const int nc = chunks_of(pos), nb = (nc + CPB - 1) / CPB;
   if (j >= nb) return;
+  ZMI_ASTAMP(0);  // diagnostic builds (tools/attn_blk_stamps.py): 0 start, 1 q in LDS, 2 scores, 3 block maxima
+                  // exchanged, 4 P, 5 P.V (V landed), 6 partial out, 7 end (the last arriver: merge done)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c16 = lane & 15, h4 = lane >> 4;
   const int key0 = j * BLK;
@@ -404,6 +406,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (wave == 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   }
   __syncthreads();  // q in LDS
+  ZMI_ASTAMP(1);
   // ---- scores (the chunked kernel's chain per 16-key sub-tile); keys past the position are -inf ----
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -424,6 +427,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
   }
   __syncthreads();
+  ZMI_ASTAMP(2);
   // ---- V^T fragments of the wave's two tiles (issued now, landing while the block maxima are exchanged) ----
   uint4 vf[2][8];
 #pragma unroll
@@ -463,6 +467,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (lane < G) mj[lane] = m;
   }
   __syncthreads();
+  ZMI_ASTAMP(3);
   // ---- e = exp(s - M_j), l per (chunk, head) as the chunked kernel's wave does it, P = bf16(e) ----
   for (int task = wave; task < CPB * G; task += BNW) {
     const int cc = task / G, g = task - cc * G;
@@ -479,6 +484,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (lane == 0) lch[cc][g] = l;
   }
   __syncthreads();
+  ZMI_ASTAMP(4);
   // ---- P.V per 32-key tile (V of keys past the position zeroed) ----
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -507,6 +513,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
   }
   __syncthreads();
+  ZMI_ASTAMP(5);
   // ---- the block's partial: chunks' tiles in tile order, then the chunks in chunk order ----
   float* po = a.part_o + ((size_t)unit * a.nch + j) * G * HD;
   float* plm = a.part_lm + ((size_t)unit * a.nch + j) * G * 2;
@@ -530,8 +537,15 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       st_wt(plm + 2 * g + 1, mj[g]);
     }
   }
-  if (nb == 1) return;
-  if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nb, &last_flag)) return;
+  ZMI_ASTAMP(6);
+  if (nb == 1) {
+    ZMI_ASTAMP(7);
+    return;
+  }
+  if (!zmi_last_arriver_wt(a.tickets + unit, (unsigned)nb, &last_flag)) {
+    ZMI_ASTAMP(7);
+    return;
+  }
   for (int e = t; e < nb * G; e += BNT) st_wt64(gu + e, 0ull);  // re-arm (every block has read its maxima)
   if (t == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -559,6 +573,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     dst[e] = (bf16_t)f2bf(acc * (1.0f / l));
   }
+  ZMI_ASTAMP(7);
 }
 
 // third launch of variant 3: one 64-thread workgroup per (unit, query head), 2 dims per thread, the unit's chunk

@@ -55,6 +55,7 @@ struct AttnArgs {
   unsigned long long* stamps;  // diagnostic build only
   ZmiPrefetch pf;      // chunked kernel, one-launch form: prefetch-only workgroups after the n_att chunk ones
   int n_att, n_pf;
+  int xc_l2;           // zmi_attn_block chunk-split form: hand-offs inside a unit through the XCD's L2 (ZMI_OPT_XC_HANDOFF)
 };
 
 __device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_t c) {

@@ -36,6 +36,18 @@ using namespace zmi_attn;
 constexpr int QG = 2, QW = 4, QNL = 8, QRT = 16;  // the projection role's gemv_body shape
 static_assert(QG * QW == DNW, "both roles run the same block size");
 constexpr int XG = 4;                         // query heads per kv head
+// the chunk-split form's hand-offs between the chunk workgroups of one (row, kv head) unit, which the grid places
+// on one XCD (blocks 8 apart; zmi_xcd_dealing checks the dealing). l2 (ZMI_OPT_XC_HANDOFF 0): a workgroup-scope
+// store keeps the line in that XCD's L2, where the consumers' agent-scope (L2-served) polls find it, instead of
+// writing it through to memory and dropping it from L2 (tools/hop_probe.hip: 228 against 449 ns per hop idle; C2
+// step 947 -> 924 us). The {value, tag} granules are unchanged, so either form gives the same bits.
+__device__ __forceinline__ void st_xc64(uint64_t* p, uint64_t v, int l2) {
+  if (l2)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    st_wt64(p, v);
+}
+
 constexpr int QKV_GRAN = (XG + 2) * HD / 2;   // q pairs | k pairs | v pairs per (row, kv head)
 constexpr int XC_CH_MAX = 24;                 // widest chunk-split form (chunk workgroups per unit)
 // its granules (layout below: maxima, l, M_j, P.V partials), then the fused out_proj role's output granules and
@@ -935,7 +947,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
       for (int g = 0; g < XG; ++g) m[g] = wave_max(m[g]);
       if (lane < XG) {
         const float mine = lane == 0 ? m[0] : (lane == 1 ? m[1] : (lane == 2 ? m[2] : m[3]));
-        st_wt64(gx + XC_GM + c * XG + lane, (uint64_t)__float_as_uint(mine) | tag64);
+        st_xc64(gx + XC_GM + c * XG + lane, (uint64_t)__float_as_uint(mine) | tag64, a.xc_l2);
       }
       const int j = c / CPB, dep = min((j + 1) * CPB, nc);
       float v = -INFINITY;
@@ -981,8 +993,8 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
       }
       l = wave_sum(l);
       if (lane == 0) {
-        st_wt64(gx + XC_GL + c * XG + wave, (uint64_t)__float_as_uint(l) | tag64);
-        st_wt64(gx + XC_GB + c * XG + wave, (uint64_t)__float_as_uint(M) | tag64);
+        st_xc64(gx + XC_GL + c * XG + wave, (uint64_t)__float_as_uint(l) | tag64, a.xc_l2);
+        st_xc64(gx + XC_GB + c * XG + wave, (uint64_t)__float_as_uint(M) | tag64, a.xc_l2);
       }
     }
     __syncthreads();
@@ -1020,7 +1032,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
 #pragma unroll
       for (int w = 1; w < CPG; ++w)
         if (CPG * c + w < n32) o += opart[w][g][d];
-      st_wt64(gx + XC_GO + (c * XG + g) * HD + d, (uint64_t)__float_as_uint(o) | tag64);
+      st_xc64(gx + XC_GO + (c * XG + g) * HD + d, (uint64_t)__float_as_uint(o) | tag64, a.xc_l2);
     }
     ZMI_ASTAMP(5);
   }
@@ -1233,6 +1245,7 @@ int attn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, uns
   at.out = (bf16_t*)attn_out;
   at.ldo = ldo;
   at.err = err;
+  at.xc_l2 = zmi_option(ZMI_OPT_XC_HANDOFF) == 0 ? 1 : 0;
   // diagnostic builds (-DZMI_ATTN_STAMPS -DZMI_GEMV_STAMPS): both roles stamp into qkv->diag, indexed
   // by block (tools/attnblk_stamps.py)
   at.stamps = a.diag ? reinterpret_cast<unsigned long long*>(a.diag) + (size_t)a.reserved * 4096 * 8 : nullptr;

@@ -19,11 +19,11 @@ int zmi_fail_msg(const char* msg) {
 
 extern "C" const char* zmi_last_error(void) { return g_err; }
 // 4: zmi_dac_conv / conv_t / conv_out take channel-blocked multi-tap weights [tap][ci / 32][co][32] (round 5), the
-//    ZMI_OPT_GEMM_ROWS bit meanings of round 5
-extern "C" int zmi_version(void) { return 4; }
+//    ZMI_OPT_GEMM_ROWS bit meanings of round 5; 5: ZMI_OPT_XC_HANDOFF (option 2) and zmi_xcd_dealing (round 6)
+extern "C" int zmi_version(void) { return 5; }
 
 // launch-geometry knobs (speed only: no option changes a result bit); defaults in the table
-static int g_opts[ZMI_OPT_COUNT] = {1, 3, 3, 0, 1, 8, 2, 1, 1, 0, 1, 256, 5, 29, 128, 0, 256, 1};
+static int g_opts[ZMI_OPT_COUNT] = {1, 3, 0, 0, 1, 8, 2, 1, 1, 0, 1, 256, 5, 29, 128, 0, 256, 1};
 int zmi_option(int which) { return (which >= 0 && which < ZMI_OPT_COUNT) ? g_opts[which] : 0; }
 extern "C" int zmi_set_option(int which, int value) {
   if (which < 0 || which >= ZMI_OPT_COUNT) return zmi_fail_msg("zmi_set_option: unknown option");
@@ -41,6 +41,37 @@ int zmi_cu_count() {
       g_cus = 256;
   }
   return g_cus;
+}
+
+namespace {
+// zmi_xcd_dealing's probe: each workgroup records the XCD it runs on (a vector store of an SGPR read)
+__global__ void xcc_kernel(unsigned* xcc) {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  if (threadIdx.x == 0) xcc[blockIdx.x] = v;
+}
+}  // namespace
+
+extern "C" int zmi_xcd_dealing(void* stream) {
+  constexpr int NB = 1024;
+  unsigned* d = nullptr;
+  unsigned h[NB];
+  hipStream_t s = (hipStream_t)stream;
+  ZMI_CHECK(hipMalloc(&d, NB * sizeof(unsigned)));
+  hipLaunchKernelGGL(xcc_kernel, dim3(NB), dim3(64), 0, s, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  ZMI_CHECK(e);
+  bool seen[8] = {};
+  for (int b = 0; b < 8; ++b) {
+    if (h[b] >= 8 || seen[h[b]]) return 0;
+    seen[h[b]] = true;
+  }
+  for (int b = 8; b < NB; ++b)
+    if (h[b] != h[b & 7]) return 0;
+  return 1;
 }
 
 namespace {

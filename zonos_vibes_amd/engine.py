@@ -38,6 +38,22 @@ def rope_table(hd: int, n: int = ROPE_TABLE_LEN) -> torch.Tensor:
     return torch.stack([cis.real, cis.imag], dim=-1).contiguous()
 
 
+_XCD_CHECKED = False
+
+
+def _check_xcd_dealing(lib, sptr):
+    """Set ZMI_OPT_XC_HANDOFF to write-through (1) unless this device deals workgroups round-robin over its XCDs."""
+    global _XCD_CHECKED
+    if _XCD_CHECKED:
+        return
+    ok = lib.zmi_xcd_dealing(sptr)
+    if ok < 0:
+        raise RuntimeError(f"zmi_xcd_dealing: {lib.zmi_last_error().decode()}")
+    if ok == 0:
+        _lib.check(lib.zmi_set_option(_lib.OPT_XC_HANDOFF, 1), "set_option")
+    _XCD_CHECKED = True
+
+
 @dataclass
 class SamplingParams:
     """Reference `sample_from_logits` keywords (sampling.py:117-129) + CFG scale + seed."""
@@ -100,6 +116,9 @@ class HipEngine:
         self.lib = _lib.lib()
         self.stream = torch.cuda.Stream(self.dev)
         self.sptr = self.stream.cuda_stream
+        # the fused attention block hands chunk maxima and partials over through the XCD's L2 (ZMI_OPT_XC_HANDOFF 0),
+        # which needs the round-robin workgroup dealing over the XCDs; checked once per process (a probe launch)
+        _check_xcd_dealing(self.lib, self.sptr)
         self.w = None
         self.attn_variant = 0  # zmi_attention_variant kernel choice (0 = library; all give identical bits)
         # decode QKV + attention as ONE launch (zmi_attn_block) where it applies: <= `attn_block_rows` rows
