@@ -26,11 +26,14 @@ def main():
     ap.add_argument("--layers", type=int, default=26)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variant", type=int, default=1)
+    ap.add_argument("--xc", type=int, default=None, help="ZMI_OPT_XC_HANDOFF (0: hand-offs through the XCD's L2)")
     ap.add_argument("--smax", type=int, default=0, help="KV capacity (default pos + 72)")
     ap.add_argument("--rezero", action="store_true", help="zero the work buffer before every launch (timing-only "
                     "builds that stop early never re-arm their hand-offs)")
     args = ap.parse_args()
     L = _lib.lib()
+    if args.xc is not None:
+        _lib.check(L.zmi_set_option(_lib.OPT_XC_HANDOFF, args.xc), "set_option")
     dev = "cuda"
     rows, p = args.rows, args.pos
     smax = args.smax or p + 72
@@ -68,7 +71,7 @@ def main():
     assert args.rezero or int(work[:4].view(torch.int32).item()) == 0, "a hand-off timed out"
     us = min(ts)
     nbytes = rows * HKV * (p + 1) * HD * 2 * 2
-    print(json.dumps(dict(lib=os.environ.get("ZMI_LIB_PATH", "default"), rows=rows, pos=p, smax=smax, variant=args.variant, rezero=args.rezero,
+    print(json.dumps(dict(lib=os.environ.get("ZMI_LIB_PATH", "default"), xc=args.xc, rows=rows, pos=p, smax=smax, variant=args.variant, rezero=args.rezero,
                           us=round(us, 2), kv_bytes=nbytes, GBps=round(nbytes / us / 1e3, 1))), flush=True)
 
 

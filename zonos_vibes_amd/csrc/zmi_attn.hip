@@ -448,7 +448,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   __syncthreads();
   uint64_t* gu = a.gran + (size_t)unit * a.nch * G;  // [block][head] in the unit's granule area
   if (wave == 0) {
-    if (nb > 1 && lane < G) st_wt64(gu + j * G + lane, pack_f2(bmx[lane], 1.0f));
+    if (nb > 1 && lane < G) st_xc64(gu + j * G + lane, pack_f2(bmx[lane], 1.0f), a.xc_l2);
     float m = lane < G ? bmx[lane] : -INFINITY;
     for (int e = lane; e < j * G; e += 64) {  // e = block x G + head (64 % G == 0: lane's head is lane % G)
       uint64_t v = ld_wt64(gu + e);
@@ -531,10 +531,10 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     if (nb == 1)  // one block: finished here (acc = ob, l = lb, as merge4 leaves them)
       dst[e] = (bf16_t)f2bf(ob * (1.0f / lb));
     else
-      st_wt(po + e, ob);
+      st_xc(po + e, ob, a.xc_l2);
     if (nb > 1 && d == 0) {
-      st_wt(plm + 2 * g, lb);
-      st_wt(plm + 2 * g + 1, mj[g]);
+      st_xc(plm + 2 * g, lb, a.xc_l2);
+      st_xc(plm + 2 * g + 1, mj[g], a.xc_l2);
     }
   }
   ZMI_ASTAMP(6);
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(BNT) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     ZMI_ASTAMP(7);
     return;
   }
-  for (int e = t; e < nb * G; e += BNT) st_wt64(gu + e, 0ull);  // re-arm (every block has read its maxima)
+  for (int e = t; e < nb * G; e += BNT) st_xc64(gu + e, 0ull, a.xc_l2);  // re-arm (every block has read its maxima)
   if (t == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -700,7 +700,7 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
   if (g * hkv != hq) return zmi_fail_msg("attention: hq must be a multiple of hkv");
   const WorkLayout w = work_layout(n_query, g, hkv, max_pos);
   char* wb = (char*)work;
-  AttnArgs a;
+  AttnArgs a{};
   a.q = (const bf16_t*)q;
   a.ldq = ldq;
   a.k = (const bf16_t*)k_cache;
@@ -758,6 +758,9 @@ extern "C" int zmi_attention_pf(const void* q, int ldq, const void* k_cache, con
   const int64_t blocks = (int64_t)n_query * hkv * a.nch;
   if (blocks + a.n_pf > 0x7fffffff) return zmi_fail_msg("attention: grid too large");
   a.n_att = variant == 5 ? (int)((int64_t)n_query * hkv * ((a.nch + CPB - 1) / CPB)) : (int)blocks;
+  // the block form's blocks of one unit are n_units apart in the grid: on one XCD when n_units is a multiple of 8, so
+  // their maxima and partials can stay in that XCD's L2 (ZMI_OPT_XC_HANDOFF 0)
+  a.xc_l2 = variant == 5 && (n_query * hkv) % 8 == 0 && zmi_option(ZMI_OPT_XC_HANDOFF) == 0 ? 1 : 0;
   if (variant != 1 && variant != 5) a.n_pf = 0;  // the split-launch forms take no prefetch role
   hipError_t e;
   switch (g) {

@@ -36,18 +36,7 @@ using namespace zmi_attn;
 constexpr int QG = 2, QW = 4, QNL = 8, QRT = 16;  // the projection role's gemv_body shape
 static_assert(QG * QW == DNW, "both roles run the same block size");
 constexpr int XG = 4;                         // query heads per kv head
-// the chunk-split form's hand-offs between the chunk workgroups of one (row, kv head) unit, which the grid places
-// on one XCD (blocks 8 apart; zmi_xcd_dealing checks the dealing). l2 (ZMI_OPT_XC_HANDOFF 0): a workgroup-scope
-// store keeps the line in that XCD's L2, where the consumers' agent-scope (L2-served) polls find it, instead of
-// writing it through to memory and dropping it from L2 (tools/hop_probe.hip: 228 against 449 ns per hop idle; C2
-// step 947 -> 924 us). The {value, tag} granules are unchanged, so either form gives the same bits.
-__device__ __forceinline__ void st_xc64(uint64_t* p, uint64_t v, int l2) {
-  if (l2)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  else
-    st_wt64(p, v);
-}
-
+// the chunk-split form's hand-offs inside a (row, kv head) unit go through the XCD's L2 (st_xc64, zmi_common.h)
 constexpr int QKV_GRAN = (XG + 2) * HD / 2;   // q pairs | k pairs | v pairs per (row, kv head)
 constexpr int XC_CH_MAX = 24;                 // widest chunk-split form (chunk workgroups per unit)
 // its granules (layout below: maxima, l, M_j, P.V partials), then the fused out_proj role's output granules and

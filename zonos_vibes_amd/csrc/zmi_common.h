@@ -162,6 +162,23 @@ __device__ __forceinline__ uint64_t ld_wt64(const uint64_t* p) {
 __device__ __forceinline__ void st_wt64(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Hand-offs between workgroups on ONE XCD (blocks 8 apart under the round-robin dealing zmi_xcd_dealing checks):
+// with l2 (ZMI_OPT_XC_HANDOFF 0) a workgroup-scope store keeps the line in that XCD's L2, where the consumers'
+// agent-scope (L2-served) polls or post-acquire loads find it, instead of writing it through to memory and dropping
+// it from L2 (tools/hop_probe.hip: 228 against 449 ns per hop idle). Never across XCDs: such a store is not visible
+// there until the kernel ends.
+__device__ __forceinline__ void st_xc64(uint64_t* p, uint64_t v, int l2) {
+  if (l2)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_xc(float* p, float v, int l2) {
+  if (l2)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ uint64_t pack_f2(float lo, float hi) {
   return (uint64_t)__float_as_uint(lo) | ((uint64_t)__float_as_uint(hi) << 32);
 }
