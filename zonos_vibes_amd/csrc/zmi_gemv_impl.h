@@ -365,12 +365,22 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     act_rows = 0u;
     for (int r = 0; r < rows; ++r) act_rows |= (qpos[r] >= 0 ? 1u : 0u) << r;
     // (1') wave 0 polls the merge workgroups' flags of the launch's units (8 per (row, kv head); rows whose position
-    // is < 0 run no attention and contribute zero rows), sleeping between sweeps, until every unit has at least one
-    // flag up: the merges are then nearly done (64 cheap flags instead of 2048 granules while the attention runs)
+    // is < 0 run no attention and contribute zero rows), sleeping between sweeps, until a unit has a flag up (below):
+    // the merges are then nearly done (64 cheap flags instead of 2048 granules while the attention runs)
     const int n_units = rows * fz.hkv;
-    if (wave == 0) {
+#ifndef ZMI_OPROJ_FLAGS
+// how long wave 0 waits on the flags before every thread polls its granules: 1 = until ANY unit has a flag up (the
+// merges finish within ~0.4 us of each other; a granule published after the sweep is picked up by the next one), 0 =
+// until every unit has one (a flag round trip, then a granule round trip: C2 step 922 us against 902-904 with 1),
+// 2 = no wait (every thread polls from dispatch: 908) (profiles/r06_oproj_flag_wait_ab.jsonl)
+#define ZMI_OPROJ_FLAGS 1
+#endif
+#ifndef ZMI_OPROJ_SLEEP
+#define ZMI_OPROJ_SLEEP 1
+#endif
+    if (wave == 0 && ZMI_OPROJ_FLAGS != 2) {
       for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
+        bool ok = ZMI_OPROJ_FLAGS == 0;
         for (int u0 = 0; u0 < n_units; u0 += 8) {  // lane = (unit u0 + lane / 8, merge workgroup lane % 8)
           const int u = u0 + (lane >> 3), qp = u < n_units ? qpos[u / fz.hkv] : -1;
           const bool up = qp < 0 || (uint32_t)(ld_wt64(fz.gran + (size_t)(row0 * fz.hkv + u) * fz.gran_stride + fz.of_off +
@@ -380,9 +390,12 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
           f = fmaxf(f, dpp_mov<DPP_XOR1>(f));
           f = fmaxf(f, dpp_mov<DPP_XOR2>(f));
           f = fmaxf(f, dpp_mov<DPP_HALF_MIRROR>(f));
-          ok = ok && f > 0.f;
+          if (ZMI_OPROJ_FLAGS == 0)
+            ok = ok && f > 0.f;
+          else
+            ok = ok || (u < n_units && f > 0.f);
         }
-        if (__all(ok)) break;
+        if (ZMI_OPROJ_FLAGS == 0 ? __all(ok) : __any(ok)) break;
         if (spins > (1u << 18)) {
           if (lane == 0) __hip_atomic_store(fz.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -422,7 +435,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
           __hip_atomic_store(fz.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(ZMI_OPROJ_SLEEP);
       }
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
