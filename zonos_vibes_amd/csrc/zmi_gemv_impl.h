@@ -126,6 +126,9 @@ struct QkvFuse {
   int og_off = 0, of_off = 0, hkv = 0;
   const int* pos = nullptr;
   unsigned* err = nullptr;
+  // FUSE == 2 (zmi_mamba_block's in_proj role): granules of columns < l2_cols are stored workgroup-scope, kept in
+  // the XCD's L2 for a step workgroup on the same XCD (st_xc64); the others write through
+  int l2_cols = 0;
 };
 
 // (6) fused epilogues of one group's 8 columns over a row tile, run by one wave; colsum(c, r) = the
@@ -150,7 +153,8 @@ __device__ __forceinline__ void epilogue(const ZmiGemvArgs& a, const ColSum& col
         reinterpret_cast<bf16_t*>(a.out)[m * a.ldo + n] = (bf16_t)hv;
         const int pos = a.row_pos[m];
         if ((c & 1) == 0 && pos >= 0)
-          st_wt64(fz.gran + m * fz.gran_stride + (n >> 1), (uint64_t)(hv | (nb << 16)) | ((uint64_t)(unsigned)(pos + 1) << 32));
+          st_xc64(fz.gran + m * fz.gran_stride + (n >> 1), (uint64_t)(hv | (nb << 16)) | ((uint64_t)(unsigned)(pos + 1) << 32),
+                  n < fz.l2_cols);
       }
     }
   } else if (EPI == ZMI_EPI_STORE || EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_F32 || EPI == ZMI_EPI_LOGITS) {

@@ -53,12 +53,27 @@ constexpr unsigned SPIN = 1u << 20;
 
 __global__ __launch_bounds__(NT) void mamba_block_kernel(const ZmiGemvArgs ia, int n_cb, int n_in,
                                                          const ZmiMamba2Args ma, uint64_t* gran, int gstride,
-                                                         unsigned* err, const ZmiPrefetch pf, int n_pf) {
+                                                         unsigned* err, const ZmiPrefetch pf, int n_pf, int xc_l2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   if (b < n_in) {
-    zmi_gemv::gemv_body<IG, IW, INL, IRT, zmi_gemv::PRO_ADDLN, ZMI_EPI_STORE, 1, 2>(
-        ia, n_cb, 1, b, smem, zmi_gemv::QkvFuse{gran, gstride});
+    zmi_gemv::QkvFuse fz{gran, gstride};
+    int cb = b;
+    if (xc_l2) {
+      // XCD-local column blocks (blocks 8 apart share an XCD, as the step workgroup of head h does: XCD h mod 8): the
+      // first 3 x 8 blocks take the B / C / dt column blocks (every head needs them: written through, and dispatched
+      // first so they land early); then block 8 (3 + 8 i + k) + x takes z (k < 4) or x (k >= 4) column block k mod 4
+      // of head x + 8 i, whose granules stay in that XCD's L2 for the head's step workgroup
+      const int x = b & 7, j = b >> 3;
+      if (j < 3) {
+        cb = 2 * ma.d_ssm / (8 * IG) + 8 * j + x;
+      } else {
+        const int i = (j - 3) >> 3, k = (j - 3) & 7, h = x + 8 * i;
+        cb = (k < 4 ? 0 : ma.d_ssm / (8 * IG)) + (MB_HD / (8 * IG)) * h + (k & 3);
+      }
+      fz.l2_cols = 2 * ma.d_ssm;
+    }
+    zmi_gemv::gemv_body<IG, IW, INL, IRT, zmi_gemv::PRO_ADDLN, ZMI_EPI_STORE, 1, 2>(ia, n_cb, 1, cb, smem, fz);
     return;
   }
   const int n_step = ma.M * ma.nheads;
@@ -155,6 +170,11 @@ extern "C" int zmi_mamba_block_pf(const ZmiGemvArgs* in_proj, const ZmiMamba2Arg
     return zmi_fail_msg("mamba_block: missing buffers");
   const int n_cb = a.N / 8 / IG;
   const int n_in = (n_cb + 7) / 8 * 8;
+  // XCD-local x / z hand-offs (ZMI_OPT_XC_HANDOFF 0): the in_proj blocks' column-block map covers exactly the
+  // Mamba2 geometry of every hybrid config this library takes (64 heads x 64 dims: 3 x 8 blocks of B / C / dt, then
+  // 8 x 8 x 8 of z / x)
+  const int xc_l2 = zmi_option(ZMI_OPT_XC_HANDOFF) == 0 && IG == 2 && s.nheads == 64 && n_in == 8 * (3 + 64) &&
+                    (2 * s.d_ssm + 2 * MB_DS + s.nheads) / 16 - 2 * s.d_ssm / 16 <= 24 ? 1 : 0;
   const size_t lds = std::max(zmi_gemv::Img<2048>::bytes(a.M, IG * IW, IRT, zmi_gemv::PRO_ADDLN), (size_t)2560);
   if (lds > zmi_gemv::LDS_MAX) return zmi_fail_msg("mamba_block: LDS image too large");
   if (lds > 64 * 1024) {
@@ -170,7 +190,7 @@ extern "C" int zmi_mamba_block_pf(const ZmiGemvArgs* in_proj, const ZmiMamba2Arg
   }
   const int n_pf = (pf.bytes[0] > 0 || pf.bytes[1] > 0) ? pf.blocks : 0;
   hipLaunchKernelGGL(mamba_block_kernel, dim3((unsigned)(n_in + a.M * s.nheads + n_pf)), dim3(NT), lds,
-                     (hipStream_t)stream, a, n_cb, n_in, s, (uint64_t*)gran, a.N / 2, err, pf, n_pf);
+                     (hipStream_t)stream, a, n_cb, n_in, s, (uint64_t*)gran, a.N / 2, err, pf, n_pf, xc_l2);
   ZMI_CHECK(hipGetLastError());
   return 0;
 }
