@@ -146,7 +146,8 @@ int64_t zmi_attn_block_gran_words(int rows, int hkv);
 /* zmi_attn_block plus `blocks` prefetch-only workgroups that read ptr[0..1][0 .. bytes) once during the
  * attention phase (HBM is nearly idle there): the next launches' weights (out_proj, the head of fc1) are
  * then served from the Infinity Cache. Results are those of zmi_attn_block; `sink` is a scratch word the
- * prefetch may write (never read). */
+ * prefetch may write (never read); `reserved` > 0 delays each prefetch workgroup's first load by that many 10 ns
+ * ticks after its start. */
 typedef struct ZmiPrefetch {
   const void* ptr[2];
   int64_t bytes[2];
@@ -374,9 +375,8 @@ const char* zmi_last_error(void);
 int zmi_version(void);
 /* 1 if this device deals a launch's workgroups round-robin over its XCDs (blocks b and b + 8 on one XCD, 8
  * distinct XCDs), 0 if not, negative on a launch error (zmi_last_error). Runs a probe launch and waits for it:
- * call it outside graph capture. The fused attention block's chunk workgroups of one (row, kv head) hand their
- * maxima and partials over through that XCD's L2 (ZMI_OPT_XC_HANDOFF 0) only where this holds; the engine calls it
- * once and sets ZMI_OPT_XC_HANDOFF to 1 otherwise. */
+ * call it outside graph capture. Hand-offs through an XCD's L2 (ZMI_OPT_XC_HANDOFF 0) rely on this; the engine
+ * calls it once per process and sets ZMI_OPT_XC_HANDOFF to 1 otherwise. */
 int zmi_xcd_dealing(void* stream);
 /* Launch-geometry knobs of the library (process-wide; speed only, no option changes a result):
  *   ZMI_OPT_GEMV_SPREAD (default 1): single-tile GEMV launches reserve enough LDS per workgroup that the
@@ -386,7 +386,14 @@ int zmi_xcd_dealing(void* stream);
  *   32-column tile loop; 0 = always the tile loop; bit 1: the dense-pair MFMA forms of the many-row form and of
  *   zmi_gemv_splitk (16 real columns per MFMA instead of 8, same bits; 1 = the M8 forms).
  *   ZMI_OPT_GEMV_SPREAD > 1: at most that many single-tile GEMV workgroups per CU (an occupancy probe).
- *   Options 2..9: reserved (knobs of the fused / persistent decode forms measured slower and removed in round 6;
+ *   ZMI_OPT_XC_HANDOFF (default 0): hand-offs between workgroups the grid places on one XCD (blocks 8 apart under
+ *          the round-robin dealing zmi_xcd_dealing checks): the chunk-split fused attention block's chunk maxima,
+ *          l / M_j and P.V partials inside a (row, kv head) unit, the block-form attention's block maxima and
+ *          partials, and zmi_mamba_block's z / x granules for the step workgroups of their head. 0 = workgroup-scope
+ *          stores that keep the lines in that XCD's L2, where the consumers' agent-scope polls read them; 1 =
+ *          write-through (agent-scope) stores, correct whatever the dealing (set where zmi_xcd_dealing returns 0).
+ *          Speed only: either gives the same bits.
+ *   Options 3..9: reserved (knobs of the fused / persistent decode forms measured slower and removed in round 6;
  *          their sources are on the git branch diag-forms).
  *   ZMI_OPT_DAC_WIDE (default 1): DAC convs on 256-row time tiles (512-thread workgroups) when the output has at
  *          least ZMI_OPT_DAC_WIDE_MIN (default 256) 256-row x 32-channel units; 0 = always 128-row tiles, 2 = always
