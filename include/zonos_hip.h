@@ -43,7 +43,7 @@ enum { ZMI_PACK_IDENTITY = 0, ZMI_PACK_SWIGLU = 1 };
  *          (res_out must not alias aux: other workgroups still read aux);
  *   GRMS   mamba-ssm RMSNormGated(X, z) * ln_w (norm_before_gate=False, one group), aux = the f32 gate
  *          z * sigmoid(z) (zmi_mamba2_step's gz), at most 4 rows. */
-enum { ZMI_PRO_AUTO = 0, ZMI_PRO_ADDLN = 2, ZMI_PRO_GRMS = 3 };
+enum { ZMI_PRO_AUTO = 0, ZMI_PRO_ADDLN = 2, ZMI_PRO_GRMS = 3, ZMI_PRO_GRMS_G = 4 };
 
 typedef struct ZmiGemvArgs {
   const void* W;        /* packed weight (zmi_pack_weight, layout M8)                          */
@@ -66,7 +66,7 @@ typedef struct ZmiGemvArgs {
   void* diag;           /* NULL; diagnostic builds only (-DZMI_GEMV_STAMPS): phase stamps       */
   int pro;              /* ZMI_PRO_*                                                            */
   int ld_aux;           /* row stride of aux and res_out (elements)                             */
-  const void* aux;      /* ADDLN: bf16 residual rows; GRMS: f32 gate rows z * sigmoid(z)          */
+  const void* aux;      /* ADDLN: bf16 residual rows; GRMS: f32 gate rows z * sigmoid(z); GRMS_G: f32 rows g = y * gate (X unused) */
   void* res_out;        /* ADDLN: bf16 [M][ld_aux] new residual, or NULL                         */
 } ZmiGemvArgs;
 
@@ -146,8 +146,7 @@ int64_t zmi_attn_block_gran_words(int rows, int hkv);
 /* zmi_attn_block plus `blocks` prefetch-only workgroups that read ptr[0..1][0 .. bytes) once during the
  * attention phase (HBM is nearly idle there): the next launches' weights (out_proj, the head of fc1) are
  * then served from the Infinity Cache. Results are those of zmi_attn_block; `sink` is a scratch word the
- * prefetch may write (never read); `reserved` > 0 delays each prefetch workgroup's first load by that many 10 ns
- * ticks after its start. */
+ * prefetch may write (never read). */
 typedef struct ZmiPrefetch {
   const void* ptr[2];
   int64_t bytes[2];
@@ -315,7 +314,7 @@ typedef struct ZmiMamba2Args {
   void* conv_ring;      /* bf16 [rows][d_conv][d_ssm + 2 d_state]: raw xBC of position q in slot q % 4 */
   void* ssm;            /* bf16 [rows][nheads][headdim][d_state]                                    */
   void* y;              /* bf16 [M][ldy] out: C.h + D x (before the gated norm)                      */
-  int ldy, reserved;
+  int ldy, gz_g;        /* gz_g: 1 = gz receives g = y * gate (for ZMI_PRO_GRMS_G), 0 = the gate     */
   const int* row_pos;   /* [M] position of the row's token (< 0: inactive row; step only)           */
   const int* row_kv;    /* [M] state row of each activation row (NULL: row m)                       */
   float* gz;            /* step only, optional: f32 [M][ldy] the gate z * sigmoid(z) of RMSNormGated */
@@ -370,7 +369,7 @@ int zmi_graph_destroy(void* graph_exec);
 const char* zmi_last_error(void);
 /* ABI version, bumped whenever a weight layout or an option's meaning changes: 4 = channel-blocked DAC conv weights
  * [tap][ci / 32][co][32] (zmi_dac_conv / conv_t / conv_out) and the round-5 ZMI_OPT_GEMM_ROWS bits; 5 =
- * ZMI_OPT_XC_HANDOFF and zmi_xcd_dealing. Check it before packing weights (zonos_vibes_amd/_lib.py refuses a library
+ * ZMI_OPT_XC_HANDOFF and zmi_xcd_dealing; 6 = ZMI_PRO_GRMS_G and ZmiMamba2Args.gz_g. Check it before packing weights (zonos_vibes_amd/_lib.py refuses a library
  * whose version differs). */
 int zmi_version(void);
 /* 1 if this device deals a launch's workgroups round-robin over its XCDs (blocks b and b + 8 on one XCD, 8

@@ -58,7 +58,7 @@ def main():
                 n_in = ((ia.N // (8 * args.ig)) + 7) // 8 * 8
             pending_out = layer < args.layers
             layer += 1
-        elif kind == "gemv" and item[0].pro == 3 and pending_out:  # the GRMS out_proj after a stamped block
+        elif kind == "gemv" and item[0].pro in (3, 4) and pending_out:  # the GRMS out_proj after a stamped block
             item[0].reserved, item[0].diag = slot, buf.data_ptr()
             names.append((f"L{layer - 1}.out_proj_grms", False))
             slot += 1

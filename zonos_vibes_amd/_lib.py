@@ -31,7 +31,7 @@ OPT_SPLITK_WGS = 16
 OPT_SPLITK_STAGE = 17
 ATTNBLK_SELF, ATTNBLK_SPLIT = 256, 512  # zmi_attn_block slices flags: self-scoring / chunk-split forms
 PACK_IDENTITY, PACK_SWIGLU = 0, 1
-PRO_AUTO, PRO_ADDLN, PRO_GRMS = 0, 2, 3
+PRO_AUTO, PRO_ADDLN, PRO_GRMS, PRO_GRMS_G = 0, 2, 3, 4
 
 
 class GemvArgs(ctypes.Structure):
@@ -85,7 +85,7 @@ class Mamba2Args(ctypes.Structure):
         ("d_ssm", c_int), ("nheads", c_int), ("headdim", c_int), ("d_state", c_int), ("d_conv", c_int),
         ("ngroups", c_int),
         ("conv_w", c_void_p), ("conv_b", c_void_p), ("dt_bias", c_void_p), ("A", c_void_p), ("D", c_void_p),
-        ("conv_ring", c_void_p), ("ssm", c_void_p), ("y", c_void_p), ("ldy", c_int), ("reserved", c_int),
+        ("conv_ring", c_void_p), ("ssm", c_void_p), ("y", c_void_p), ("ldy", c_int), ("gz_g", c_int),
         ("row_pos", c_void_p), ("row_kv", c_void_p), ("gz", c_void_p),
     ]
 
@@ -170,7 +170,7 @@ _SIGS = {
 
 EXPORTED = sorted(_SIGS)
 _lib = None
-ABI_VERSION = 5  # zmi_version() of the library this binding (and its weight packers) is written for
+ABI_VERSION = 6  # zmi_version() of the library this binding (and its weight packers) is written for
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:

@@ -53,11 +53,12 @@ extern "C" int zmi_gemv_launch(const ZmiGemvArgs* args, int epi, void* stream) {
   if (a.ldx % 8) return zmi_fail_msg("gemv: ldx must be a multiple of 8 (16-byte rows)");
   if (a.groups < 0 || a.groups > 2 || (a.groups == 2 && a.K != 2048 && a.K != 8192))
     return zmi_fail_msg("gemv: groups must be 0 (library choice), 1, or 2 for K = 2048 / 8192");
-  if (a.pro != ZMI_PRO_AUTO && a.pro != ZMI_PRO_ADDLN && a.pro != ZMI_PRO_GRMS) return zmi_fail_msg("gemv: unknown prologue");
+  if (a.pro != ZMI_PRO_AUTO && a.pro != ZMI_PRO_ADDLN && a.pro != ZMI_PRO_GRMS && a.pro != ZMI_PRO_GRMS_G)
+    return zmi_fail_msg("gemv: unknown prologue");
   if (a.pro == ZMI_PRO_ADDLN && (!a.ln_w || !a.ln_b || !a.aux || a.ld_aux % 8 || a.res_out == a.aux))
     return zmi_fail_msg("gemv: ADDLN needs ln_w, ln_b, aux (ld_aux % 8 == 0) and res_out != aux");
-  if (a.pro == ZMI_PRO_GRMS && (!a.ln_w || !a.aux || a.ld_aux % 8 || a.M > 4))
-    return zmi_fail_msg("gemv: GRMS needs ln_w (the norm weight), aux = the f32 gate (ld_aux % 8 == 0), M <= 4");
+  if ((a.pro == ZMI_PRO_GRMS || a.pro == ZMI_PRO_GRMS_G) && (!a.ln_w || !a.aux || a.ld_aux % 8 || a.M > 4))
+    return zmi_fail_msg("gemv: GRMS needs ln_w (the norm weight), aux = the f32 gate or g rows (ld_aux % 8 == 0), M <= 4");
   if (epi == ZMI_EPI_QKV && (a.hd % 8 || a.smax <= 0 || !a.row_pos || !a.row_kv || !a.rope))
     return zmi_fail_msg("gemv: the QKV epilogue needs row_pos, row_kv, rope, smax and hd % 8 == 0");
   hipStream_t s = (hipStream_t)stream;

@@ -32,6 +32,9 @@
 namespace zmi_gemv {
 
 constexpr int PRO_PLAIN = 0, PRO_LN = 1, PRO_ADDLN = 2, PRO_GRMS = 3;
+// GRMSG: RMSNormGated from aux rows that already hold g = y * gate (f32): no y rows staged (zmi_mamba_block's step
+// writes g; the same bits as GRMS, one third fewer activation bytes per workgroup)
+constexpr int PRO_GRMSG = 4;
 constexpr size_t LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
 // DPP row_ror:8 — lane i of each 16-lane row reads lane (i + 8) & 15 of the same row
@@ -61,8 +64,9 @@ struct Img {
   static constexpr int XROW = K + 8;
   static constexpr int GROW = K + 8;  // f32 gate rows (GRMS)
   static size_t bytes(int rows, int nwv, int rt, int pro) {
-    const size_t gb = (pro == PRO_LN || pro == PRO_ADDLN) ? (size_t)4 * K : (pro == PRO_GRMS ? (size_t)2 * K : 0);
-    const size_t aux = pro == PRO_ADDLN ? (size_t)rows * XROW * 2 : (pro == PRO_GRMS ? (size_t)rows * GROW * 4 : 0);
+    const bool grms = pro == PRO_GRMS || pro == PRO_GRMSG;
+    const size_t gb = (pro == PRO_LN || pro == PRO_ADDLN) ? (size_t)4 * K : (grms ? (size_t)2 * K : 0);
+    const size_t aux = pro == PRO_ADDLN ? (size_t)rows * XROW * 2 : (grms ? (size_t)rows * GROW * 4 : 0);
     return (size_t)rows * XROW * 2 + aux + gb + (size_t)nwv * 8 * rt * 4;
   }
 };
@@ -259,13 +263,14 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   const int rt_end = min(n_rt, rt + rpw);
   int row0 = rt * RT;
   int rows = min(RT, a.M - row0);
-  constexpr bool AUX = PRO == PRO_ADDLN || PRO == PRO_GRMS;
-  constexpr int GB = (PRO == PRO_LN || PRO == PRO_ADDLN) ? 2 : (PRO == PRO_GRMS ? 1 : 0);  // gamma / beta rows
+  constexpr bool GRMS = PRO == PRO_GRMS || PRO == PRO_GRMSG;
+  constexpr bool AUX = PRO == PRO_ADDLN || GRMS;
+  constexpr int GB = (PRO == PRO_LN || PRO == PRO_ADDLN) ? 2 : (GRMS ? 1 : 0);  // gamma / beta rows
   constexpr int GROW = Img<K>::GROW;
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
   bf16_t* xa = xs + (size_t)alloc_rows * XROW;  // aux rows: ADDLN bf16 residual, GRMS f32 gate
   float* xg = reinterpret_cast<float*>(xa);
-  bf16_t* gam = xa + (PRO == PRO_ADDLN ? (size_t)alloc_rows * XROW : (PRO == PRO_GRMS ? (size_t)alloc_rows * GROW * 2 : 0));
+  bf16_t* gam = xa + (PRO == PRO_ADDLN ? (size_t)alloc_rows * XROW : (GRMS ? (size_t)alloc_rows * GROW * 2 : 0));
   bf16_t* bet = gam + K;
   float* red = reinterpret_cast<float*>(gam + (size_t)GB * K);
 
@@ -293,11 +298,11 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   // the current tile's reduction and epilogue
   auto stage_rows = [&](bool first, int s_row0, int s_rows, const bf16_t* s_X) {
     constexpr int PPR = K / 512;
-    const int n_x = s_rows * PPR;
-    constexpr int APR = PRO == PRO_GRMS ? 2 * PPR : PPR;  // aux pieces per row (f32 gate rows: twice the bytes)
+    const int n_x = PRO == PRO_GRMSG ? 0 : s_rows * PPR;  // GRMSG: no y rows
+    constexpr int APR = GRMS ? 2 * PPR : PPR;  // aux pieces per row (f32 gate rows: twice the bytes)
     const int n_a = AUX ? s_rows * APR : 0;
     const int n_pc = n_x + n_a + (first ? GB * PPR : 0);
-    const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)s_row0 * a.ld_aux * (PRO == PRO_GRMS ? 2 : 1)
+    const bf16_t* XA = AUX ? reinterpret_cast<const bf16_t*>(a.aux) + (size_t)s_row0 * a.ld_aux * (GRMS ? 2 : 1)
                            : nullptr;
     for (int pc = wave; pc < n_pc; pc += NWV) {
       if (pc < n_x) {
@@ -305,7 +310,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
         dma_piece(s_X + (size_t)r * a.ldx + p * 512 + lane * 8, xs + r * XROW + p * 512);
       } else if (pc < n_x + n_a) {
         const int r = (pc - n_x) / APR, p = (pc - n_x) - r * APR;
-        if (PRO == PRO_GRMS)  // 1 KiB = 256 f32 of the gate row
+        if (GRMS)  // 1 KiB = 256 f32 of the gate (GRMSG: g) row
           dma_piece(XA + ((size_t)r * a.ld_aux + p * 256) * 2 + lane * 8,
                     reinterpret_cast<bf16_t*>(xg + r * GROW + p * 256));
         else
@@ -607,7 +612,7 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
     }
     __syncthreads();
   }
-  if (PRO == PRO_GRMS) {
+  if (GRMS) {
     // RMSNormGated (norm_before_gate=False): g = y (z sigmoid(z)), out = g rstd w; g recomputed in the
     // apply pass (the same bits), sums of g^2 element by element as zmi_gated_rmsnorm. A wave takes its
     // (row, part) tasks two at a time (the second clamped, its results dropped): two independent dependent-add
@@ -627,13 +632,16 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
         t[u] = 0.f;
 #pragma unroll
         for (int i = 0; i < CPQ; ++i) {
-          const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
-          const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
+          uint32_t y[4] = {0u, 0u, 0u, 0u};
+          if constexpr (PRO == PRO_GRMS) {
+            const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+            y[0] = yv.x; y[1] = yv.y; y[2] = yv.z; y[3] = yv.w;
+          }
           float gz[8];
           load_gate(zr + (lane + 64 * i) * 8, gz);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float g = gate_elem(y, gz, e);
+            const float g = PRO == PRO_GRMSG ? gz[e] : gate_elem(y, gz, e);
             t[u] += g * g;
           }
         }
@@ -658,17 +666,20 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
 #pragma unroll
         for (int i = 0; i < CPQ; ++i) {
           const int c = q * (K / NQ) / 8 + lane + 64 * i;
-          const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+          uint32_t y[4] = {0u, 0u, 0u, 0u};
+          if constexpr (PRO == PRO_GRMS) {
+            const uint4 yv = *reinterpret_cast<const uint4*>(yr + (lane + 64 * i) * 8);
+            y[0] = yv.x; y[1] = yv.y; y[2] = yv.z; y[3] = yv.w;
+          }
           const uint4 gw = *reinterpret_cast<const uint4*>(gam + c * 8);
-          const uint32_t y[4] = {yv.x, yv.y, yv.z, yv.w};
           const uint32_t uw[4] = {gw.x, gw.y, gw.z, gw.w};
           float gz[8];
           load_gate(zr + (lane + 64 * i) * 8, gz);
+          auto gv = [&](int e) { return PRO == PRO_GRMSG ? gz[e] : gate_elem(y, gz, e); };
           uint32_t o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            o[j] = f2bf((gate_elem(y, gz, 2 * j) * rstd) * bf2f(uw[j])) |
-                   (f2bf((gate_elem(y, gz, 2 * j + 1) * rstd) * bf2f(uw[j] >> 16)) << 16);
+            o[j] = f2bf((gv(2 * j) * rstd) * bf2f(uw[j])) | (f2bf((gv(2 * j + 1) * rstd) * bf2f(uw[j] >> 16)) << 16);
           res[u][i] = uint4{o[0], o[1], o[2], o[3]};
         }
       }
@@ -1078,6 +1089,11 @@ hipError_t launch_g(const ZmiGemvArgs& a, hipStream_t s) {
   if (a.pro == ZMI_PRO_GRMS) {  // the Mamba2 out_proj (K = d_ssm)
     if constexpr ((K == 1024 || K == 4096) && EPI == ZMI_EPI_STORE)
       return once ? launch_p<G, W, NL, RT, PRO_GRMS, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_GRMS, EPI, 0>(a, s);
+    return hipErrorInvalidValue;
+  }
+  if (a.pro == ZMI_PRO_GRMS_G) {  // the same from g = y * gate rows (decode: one tile)
+    if constexpr ((K == 1024 || K == 4096) && EPI == ZMI_EPI_STORE)
+      return once ? launch_p<G, W, NL, RT, PRO_GRMSG, EPI, 1>(a, s) : hipErrorInvalidValue;
     return hipErrorInvalidValue;
   }
   if (ln) return once ? launch_p<G, W, NL, RT, PRO_LN, EPI, 1>(a, s) : launch_p<G, W, NL, RT, PRO_LN, EPI, 0>(a, s);

@@ -133,10 +133,13 @@ __device__ __forceinline__ void step_core(const ZmiMamba2Args& a, int m, int h, 
   for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = pre.sv[j];
   out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
   if (nq == 0) {
-    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)f2bf(out + x * pre.D);
-    if (a.gz) {  // RMSNormGated's gate of this channel, once (the out_proj GEMV's GRMS prologue multiplies)
+    const uint32_t yb = f2bf(out + x * pre.D);
+    reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)yb;
+    if (a.gz) {  // RMSNormGated's gate of this channel, once (the out_proj GEMV's GRMS prologue multiplies), or (gz_g)
+                 // g = y * gate itself, the product gate_elem forms (GRMS_G: the out_proj then stages no y rows)
       const float zz = bf2f(raw[RAW_Z + p]);
-      a.gz[(size_t)m * a.ldy + h * MB_HD + p] = zz * (1.0f / (1.0f + expf(-zz)));
+      const float gate = zz * (1.0f / (1.0f + expf(-zz)));
+      a.gz[(size_t)m * a.ldy + h * MB_HD + p] = a.gz_g ? bf2f(yb) * gate : gate;
     }
   }
 }

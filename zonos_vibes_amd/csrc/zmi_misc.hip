@@ -19,8 +19,9 @@ int zmi_fail_msg(const char* msg) {
 
 extern "C" const char* zmi_last_error(void) { return g_err; }
 // 4: zmi_dac_conv / conv_t / conv_out take channel-blocked multi-tap weights [tap][ci / 32][co][32] (round 5), the
-//    ZMI_OPT_GEMM_ROWS bit meanings of round 5; 5: ZMI_OPT_XC_HANDOFF (option 2) and zmi_xcd_dealing (round 6)
-extern "C" int zmi_version(void) { return 5; }
+//    ZMI_OPT_GEMM_ROWS bit meanings of round 5; 5: ZMI_OPT_XC_HANDOFF (option 2) and zmi_xcd_dealing (round 6);
+//    6: ZMI_PRO_GRMS_G and ZmiMamba2Args.gz_g (round 6)
+extern "C" int zmi_version(void) { return 6; }
 
 // launch-geometry knobs (speed only: no option changes a result bit); defaults in the table
 static int g_opts[ZMI_OPT_COUNT] = {1, 3, 0, 0, 1, 8, 2, 1, 1, 0, 1, 256, 5, 29, 128, 0, 256, 1};

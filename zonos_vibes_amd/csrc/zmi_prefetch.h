@@ -9,10 +9,6 @@
 
 template <int NTH>
 __device__ __forceinline__ void prefetch_body(const ZmiPrefetch& pf, int j, int n_pf) {
-  if (pf.reserved > 0) {  // start delay (10 ns ticks of s_memrealtime): stay off the launch's latency chain
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)pf.reserved) __builtin_amdgcn_s_sleep(16);
-  }
   unsigned acc = 0;
 #pragma unroll
   for (int r = 0; r < 2; ++r) {

@@ -146,7 +146,6 @@ class HipEngine:
         # (256, + 4-8 MB), 966 (256, + 16 MB), 974 (512, + 8 MB) (profiles/r03_prefetch_ab.jsonl)
         self.prefetch_blocks = 256
         self.prefetch_fc1_mb = 8
-        self.prefetch_delay_us = 0.0  # start delay of those prefetch workgroups (ZmiPrefetch.reserved)
         # the same prefetch role in the separate chunked attention launch (steps of > 8 rows, positions past the
         # fused forms' reach): workgroups at the end of its grid read out_proj's weights and the first
         # `attn_prefetch_fc1_mb` MB of fc1's while the chunks exchange maxima and merge (0 blocks = off). C5-shaped
@@ -430,7 +429,6 @@ class HipEngine:
                         pf.ptr[1] = nw.data_ptr()
                         pf.bytes[1] = min(nw.numel() * 2, int(self.prefetch_fc1_mb * 2 ** 20))
                         pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
-                        pf.reserved = int(round(self.prefetch_delay_us * 100))
                     o_fused = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)[0] if oproj else None
                     plan.append(("attnblk", (qkv[0], i, pf, self._block_slices(form), o_fused)))
                 else:

@@ -91,6 +91,9 @@ class HybridEngine(HipEngine):
         # prefetch the layer's out_proj weights into the Infinity Cache during the step phase: measured slower
         # (C4 300 frames: 320 ms off; 321, 333 and 361 ms with 64, 192 and 32 prefetch workgroups), so off
         self.mamba_prefetch = False
+        # the decode out_proj's RMSNormGated prologue reads g = y * gate written by the step (GRMS_G: 32 KB of activation
+        # rows per workgroup at 2 rows) instead of y and the gate (GRMS: 48 KB); the same bits
+        self.grms_g = True
         self.prefetch_blocks, self.prefetch_fc1_mb = 192, 0  # the MHA blocks' out_proj prefetch (measured in round 2)
 
     def _kv_layers(self) -> int:
@@ -106,7 +109,7 @@ class HybridEngine(HipEngine):
             self.x2 = z(R, self.d)  # the decode residual stream ping-pongs between self.x and self.x2
             self.zero_rows = z(R, self.d)  # block 0's "hidden": s = 0 + residual, exactly the residual
             self.zx, self.yb, self.yn = z(R, md["d_in_proj"]), z(R, md["d_ssm"]), z(R, md["d_ssm"])
-            self.gz = z(R, md["d_ssm"], dt=torch.float32)  # RMSNormGated's gate z * sigmoid(z) (decode)
+            self.gz = z(R, md["d_ssm"], dt=torch.float32)  # decode: g = y * gate (grms_g) or the gate z * sigmoid(z)
             self.hid_pre, self.nrm_pre = z(2 * P, self.d), z(2 * P, self.d)
             self.zx_pre, self.yb_pre, self.yn_pre = z(2 * P, md["d_in_proj"]), z(2 * P, md["d_ssm"]), z(2 * P, md["d_ssm"])
             self.hm = z(R, max(self.Fm, self.F, 1))
@@ -316,8 +319,8 @@ class HybridEngine(HipEngine):
                                                  self.zx, md["d_in_proj"]), ln1, i == 0)
                     sa = self._mamba_args(lw, self.zx, self.yb, rows, self.row_pos, None)
                     fuse_g = rows <= 4  # the f32 gate rows of a larger tile would not fit the LDS image
-                    if fuse_g:
-                        sa.gz = self.gz.data_ptr()
+                    if fuse_g:  # the step writes g = y * gate (gz_g), the out_proj's GRMS_G prologue reads only g
+                        sa.gz, sa.gz_g = self.gz.data_ptr(), 1 if self.grms_g else 0
                     if self.mamba_block and d == 2048 and rows <= 16:
                         plan.append(("call", self._call_mamba_block(inp[1][0], sa, self.mgran[lw["st"]],
                                                                     lw["out"] if self.mamba_prefetch else None)))
@@ -328,7 +331,8 @@ class HybridEngine(HipEngine):
                     if fuse_g:
                         out[0].ln_w = lw["norm_w"].data_ptr()
                         out[0].eps = 1e-5  # RMSNormGated's own eps (mamba2.py)
-                        plan.append(self._fused(out, _lib.PRO_GRMS, self.gz, md["d_ssm"]))
+                        plan.append(self._fused(out, _lib.PRO_GRMS_G if self.grms_g else _lib.PRO_GRMS, self.gz,
+                                                md["d_ssm"]))
                     else:
                         plan.append(("call", self._gnorm(lw, self.yb, self.zx, self.yn, rows)))
                         plan.append(("gemv", self._gemv(lw["out"], self.yn, rows, d, md["d_ssm"], _lib.EPI_STORE,
