@@ -165,6 +165,7 @@ class HipEngine:
         # ... also in the 24-chunk form (batch-1 steps at positions 1024 .. 3071)
         self.attn_oproj_wide = True
         self.heads_groups = 0  # column groups of the heads GEMV (0: the library's choice)
+        self.fc1_groups = 0  # column groups of the decode fc1 GEMV (0: the library's choice, 2)
         # fc2 (K = 8192) over >= `splitk_rows` rows and out_proj (K = 2048) over >= `splitk_o_rows` rows as
         # split-K GEMMs (zmi_gemv_splitk: each column block reads the activation rows once, and the reduce can
         # write the next LayerNorm; identical bits); 0 = never. out_proj split-K: C5-shaped 16-row step 1.732 vs
@@ -444,8 +445,9 @@ class HipEngine:
                 o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_RESIDUAL, self.x, d)
                 if oproj:  # out_proj ran inside the fused block
                     xin, ln = normed((lw["ln2_w"], lw["ln2_b"]))
-                    plan.append(("gemv", self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h,
-                                                    self.F, ln=ln)))
+                    f1 = self._gemv(lw["fc1"], xin, rows, 2 * self.F, d, _lib.EPI_SWIGLU, self.h, self.F, ln=ln)
+                    f1[0].groups = self.fc1_groups
+                    plan.append(("gemv", f1))
                 else:
                     if pre and self._use_splitk(*o_item) and d == 2048:
                         # the split-K reduce also writes LayerNorm(new x) for fc1 (no pre-pass launch)
