@@ -902,7 +902,7 @@ def main():
                                     "unit": "TFLOP/s", "frac": round(dac_tf / MFMA_PEAK_TFLOPS, 4),
                                     "flop_per_frame": DAC_FLOP_PER_FRAME, "frames": n_new,
                                     "ms": breakdown["dac_decode_ms"],
-                                    "mfma_busy_source": "profiles/r05_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
+                                    "mfma_busy_source": "profiles/r06_dac_mfma_pmc.json (SQ_VALU_MFMA_BUSY_CYCLES pass)"},
             "c3_sharded": c3,
             "widened": widened,
             "end_of_batch_gather": gather,
