@@ -29,23 +29,23 @@ namespace {
 
 using namespace zmi_mamba;
 
-__global__ __launch_bounds__(MB_NT) void mamba2_step_kernel(const ZmiMamba2Args a) {
+__global__ __launch_bounds__(MB_ST) void mamba2_step_kernel(const ZmiMamba2Args a) {
   const int m = blockIdx.x / a.nheads, h = blockIdx.x - m * a.nheads;
   const int pos = a.row_pos[m];
   if (pos < 0) return;
   const int kv = a.row_kv ? a.row_kv[m] : m;
   __shared__ float xs[MB_HD], bc[2 * MB_DS];
   __shared__ bf16_t raw[RAW_N];
-  StepPre<MB_NT> pre;
-  step_prefetch<MB_NT>(a, h, pos, kv, pre);  // the state slice first: the longest loads, under the rest
+  StepPre<MB_ST> pre;
+  step_prefetch<MB_ST>(a, h, pos, kv, pre);  // the state slice first: the longest loads, under the rest
   const bf16_t* zx = reinterpret_cast<const bf16_t*>(a.zxbcdt) + (size_t)m * a.ld_zx;
-  for (int i = threadIdx.x; i < RAW_DT + 1; i += MB_NT) {
+  for (int i = threadIdx.x; i < RAW_DT + 1; i += MB_ST) {
     const int col = i < RAW_Z ? a.d_ssm + conv_channel(i, h, a.d_ssm)
                               : (i < RAW_DT ? h * MB_HD + (i - RAW_Z) : 2 * a.d_ssm + 2 * MB_DS + h);
     raw[i] = zx[col];
   }
   __syncthreads();
-  step_core<MB_NT>(a, m, h, pos, kv, raw, pre, xs, bc);
+  step_core<MB_ST>(a, m, h, pos, kv, raw, pre, xs, bc);
 }
 
 // ---------------------------------------------------------------------------- prefill scan
@@ -700,7 +700,7 @@ int check_mamba(const ZmiMamba2Args* a) {
 extern "C" int zmi_mamba2_step(const ZmiMamba2Args* a, void* stream) {
   if (int e = check_mamba(a)) return e;
   if (a->M <= 0) return 0;
-  hipLaunchKernelGGL(mamba2_step_kernel, dim3((unsigned)(a->M * a->nheads)), dim3(MB_NT), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(mamba2_step_kernel, dim3((unsigned)(a->M * a->nheads)), dim3(MB_ST), 0, (hipStream_t)stream, *a);
   ZMI_CHECK(hipGetLastError());
   return 0;
 }

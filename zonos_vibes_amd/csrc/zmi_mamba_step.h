@@ -9,7 +9,8 @@ namespace zmi_mamba {
 constexpr int MB_HD = 64;    // headdim
 constexpr int MB_DS = 128;   // d_state (ngroups = 1)
 constexpr int MB_DC = 4;     // d_conv
-constexpr int MB_NT = 256;   // threads: (p = t / 4, n-quarter = t % 4)
+constexpr int MB_NT = 256;   // threads of the prefill scan kernels: (p = t / 4, n-quarter = t % 4)
+constexpr int MB_ST = 512;   // threads of a decode step workgroup: (p = t / 8, n-eighth = t % 8)
 constexpr int MB_NCH = MB_HD + 2 * MB_DS;  // conv channels one head needs: its x, then B, C
 
 __device__ __forceinline__ float silu_f(float v) { return v / (1.0f + expf(-v)); }
@@ -41,7 +42,10 @@ constexpr int RAW_X = 0, RAW_BC = MB_HD, RAW_Z = MB_NCH, RAW_DT = MB_NCH + MB_HD
 template <int NT>
 struct StepPre {
   static constexpr int NI = (MB_NCH + NT - 1) / NT;  // conv channels per thread
-  uint4 sv[4];              // state slice (threads < 256)
+  static constexpr int PARTS = NT / MB_HD;           // threads per state row p (8 at 512 threads)
+  static constexpr int SVN = MB_DS / 8 / PARTS;      // uint4 of the state row per thread
+  static_assert(PARTS == 4 || PARTS == 8, "a state row split over 4 or 8 lanes");
+  uint4 sv[SVN];            // state slice
   float ring[NI][MB_DC - 1];
   float w[NI][MB_DC];
   float bias[NI];
@@ -51,11 +55,12 @@ struct StepPre {
 template <int NT>
 __device__ __forceinline__ void step_prefetch(const ZmiMamba2Args& a, int h, int pos, int kv, StepPre<NT>& pre) {
   const int t = threadIdx.x, conv_dim = a.d_ssm + 2 * MB_DS;
-  if (t < MB_NT) {
+  {
+    constexpr int P = StepPre<NT>::PARTS;
     const bf16_t* st = reinterpret_cast<const bf16_t*>(a.ssm) +
-                       (((size_t)kv * a.nheads + h) * MB_HD + (t >> 2)) * MB_DS + (t & 3) * 32;
+                       (((size_t)kv * a.nheads + h) * MB_HD + t / P) * MB_DS + (t % P) * (MB_DS / P);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pre.sv[j] = reinterpret_cast<const uint4*>(st)[j];
+    for (int j = 0; j < StepPre<NT>::SVN; ++j) pre.sv[j] = reinterpret_cast<const uint4*>(st)[j];
   }
   pre.dt_bias = a.dt_bias[h];
   pre.A = a.A[h];
@@ -106,16 +111,17 @@ __device__ __forceinline__ void step_core(const ZmiMamba2Args& a, int m, int h, 
   const float dtv = softplus_f(bf2f(raw[RAW_DT]) + pre.dt_bias);
   const float dA = expf(pre.A * dtv);
   __syncthreads();
-  if (t >= MB_NT) return;
-  // (3) state update and readout: lane (p, quarter) owns state[p][32 quarter .. +31]
-  const int p = t >> 2, nq = t & 3;
-  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * 32;
+  // (3) state update and readout: lane (p, part) owns state[p][MB_DS / P part .. +MB_DS / P - 1] (P = NT / 64 lanes per
+  // row p: 8 at the decode step's 512 threads, so each lane's readout chain is 16 terms long)
+  constexpr int P = StepPre<NT>::PARTS, SVN = StepPre<NT>::SVN;
+  const int p = t / P, nq = t % P;
+  bf16_t* st = reinterpret_cast<bf16_t*>(a.ssm) + (((size_t)kv * a.nheads + h) * MB_HD + p) * MB_DS + nq * (MB_DS / P);
   const float x = xs[p];
-  const float* B = bc + nq * 32;
-  const float* C = bc + MB_DS + nq * 32;
+  const float* B = bc + nq * (MB_DS / P);
+  const float* C = bc + MB_DS + nq * (MB_DS / P);
   float out = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < SVN; ++j) {
     uint32_t w[4] = {pre.sv[j].x, pre.sv[j].y, pre.sv[j].z, pre.sv[j].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -130,8 +136,9 @@ __device__ __forceinline__ void step_core(const ZmiMamba2Args& a, int m, int h, 
     pre.sv[j] = uint4{w[0], w[1], w[2], w[3]};
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) reinterpret_cast<uint4*>(st)[j] = pre.sv[j];
-  out = quad_sum(out);  // the four quarters of row p are lanes 4p .. 4p+3
+  for (int j = 0; j < SVN; ++j) reinterpret_cast<uint4*>(st)[j] = pre.sv[j];
+  out = quad_sum(out);  // the P parts of row p are lanes P p .. P p + P - 1
+  if constexpr (P == 8) out += dpp_mov<DPP_HALF_MIRROR>(out);
   if (nq == 0) {
     const uint32_t yb = f2bf(out + x * pre.D);
     reinterpret_cast<bf16_t*>(a.y)[(size_t)m * a.ldy + h * MB_HD + p] = (bf16_t)yb;

@@ -31,6 +31,7 @@ using namespace zmi_mamba;
 #endif
 constexpr int IG = ZMI_MB_IG, IW = 4, INL = 8, IRT = 16;  // in_proj role: the K = 2048 shape, IG groups
 constexpr int NT = IG * IW * 64;
+static_assert(NT == MB_ST, "the fused step role runs zmi_mamba2_step's thread layout (the same readout order)");
 constexpr int NGRAN = MB_HD / 2 + MB_DS + MB_HD / 2 + 1;  // x pairs, B / C pairs, z pairs, the dt pair
 constexpr unsigned SPIN = 1u << 20;
 
