@@ -144,7 +144,9 @@ class HipEngine:
         # first `prefetch_fc1_mb` MB of fc1's while the attention runs (speed only). With out_proj and fc1 as
         # separate launches: C2 step 971 us (192 blocks, out_proj only), 959 (192, + 8 MB of fc1), 944-947
         # (256, + 4-8 MB), 966 (256, + 16 MB), 974 (512, + 8 MB) (profiles/r03_prefetch_ab.jsonl)
-        self.prefetch_blocks = 256
+        # round 6, after the hand-offs through L2: 128 workgroups x 8 MB 896.6-899.2 us, 256 x 8 MB 905, 64 / 96 x 8 MB 903 /
+        # 905, 128 x 6 / 12 / 16 MB 903 / 906 / 919 (profiles/r06_prefetch_sizing_ab.jsonl)
+        self.prefetch_blocks = 128
         self.prefetch_fc1_mb = 8
         # the same prefetch role in the separate chunked attention launch (steps of > 8 rows, positions past the
         # fused forms' reach): workgroups at the end of its grid read out_proj's weights and the first
