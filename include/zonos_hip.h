@@ -155,8 +155,10 @@ typedef struct ZmiPrefetch {
 } ZmiPrefetch;
 int zmi_attn_block_pf(const ZmiGemvArgs* qkv, void* gran, unsigned* err, void* attn_out, int ldo, int slices,
                       const ZmiPrefetch* prefetch, void* stream);
-/* zmi_attn_block_pf with the layer's out_proj in the same launch (8-chunk split form only: slices = 8 |
- * ZMI_ATTNBLK_SPLIT, LayerNorm prologue): `oproj` holds the plain EPI_RESIDUAL GEMV arguments as for zmi_gemv_launch
+/* zmi_attn_block_pf with the layer's out_proj in the same launch (the chunk-split forms: slices = 8 or 24 |
+ * ZMI_ATTNBLK_SPLIT). With the LayerNorm prologue `oproj` holds the plain EPI_RESIDUAL GEMV arguments as for zmi_gemv_launch;
+ * with the ADDLN prologue (the hybrid's MHA blocks) the role stores bf16(out_proj) to oproj->out (EPI_STORE: the hidden
+ * rows the next block's add + LayerNorm reads; not the residual buffers). The LayerNorm case:
  * (W = out_proj weights, K = hq hd, N % 16 == 0, X = attn_out, out = the residual rows x, M = qkv->M), replacing
  * reference _torch.py:115,140 and the residual add :100. Its workgroups follow the attention ones: they load their
  * weight slice at their start and gather the attention output from the merging workgroups' {pair, tag} granules

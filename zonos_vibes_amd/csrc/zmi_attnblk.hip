@@ -1159,8 +1159,11 @@ __global__ __launch_bounds__(NT) void attn_block_kernel(const ZmiGemvArgs qa, in
       fz.hkv = at.hkv;
       fz.pos = at.pos;
       fz.err = at.err;
-      zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_PLAIN, ZMI_EPI_RESIDUAL, 1, 3>(oa, oa.N / 8 / QG, 1,
-                                                                                       b - n_qkv - n_xs, smem, fz);
+      // transformer blocks: x + bf16(out_proj) in place (_torch.py:100); the hybrid's MHA blocks (ADDLN projection):
+      // bf16(out_proj) into the hidden rows, which the next block's add + LayerNorm adds to the residual
+      constexpr int OEPI = PRO == zmi_gemv::PRO_ADDLN ? ZMI_EPI_STORE : ZMI_EPI_RESIDUAL;
+      zmi_gemv::gemv_body<QG, QW, QNL, QRT, zmi_gemv::PRO_PLAIN, OEPI, 1, 3>(oa, oa.N / 8 / QG, 1, b - n_qkv - n_xs,
+                                                                             smem, fz);
     }
   } else
     prefetch_body<NT>(pf, b - n_qkv - n_xs - n_op, n_pf);
@@ -1251,20 +1254,27 @@ int attn_block(const ZmiGemvArgs* qkv, const ZmiGemvArgs* oproj, void* gran, uns
   const int sl = slices & ~(ZMI_ATTNBLK_SELF | ZMI_ATTNBLK_SPLIT);
   if (form == FORM_SPLIT ? (sl != 8 && sl != 24) : (sl != 4 && sl != 8))
     return zmi_fail_msg("attn_block: slices must be 4 or 8 (| ZMI_ATTNBLK_SELF), or 8 or 24 | ZMI_ATTNBLK_SPLIT");
-  if (oproj) {  // the out_proj role (split forms, LayerNorm'd transformer blocks)
+  if (oproj) {  // the out_proj role (split forms; LayerNorm'd transformer blocks: residual epilogue; ADDLN hybrid MHA
+               // blocks: plain store into the hidden rows)
     const ZmiGemvArgs& o = *oproj;
-    if (form != FORM_SPLIT || addln)
-      return zmi_fail_msg("attn_block: the fused out_proj runs with the chunk-split forms and a LayerNorm prologue");
+    if (form != FORM_SPLIT)
+      return zmi_fail_msg("attn_block: the fused out_proj runs with the chunk-split forms");
     if (o.K != a.hq * a.hd || o.N % (8 * QG) || o.n_valid != o.N || o.M != a.M || o.ln_w || o.pro != ZMI_PRO_AUTO ||
         !o.out || o.ldo % 8 || o.ldo < o.N || o.X != attn_out)
       return zmi_fail_msg("attn_block: out_proj must be the plain residual GEMV over the attention output "
                           "(K = hq hd, N % 16 == 0, same rows, X = attn_out)");
+    if (addln && (o.out == a.aux || o.out == a.res_out))
+      return zmi_fail_msg("attn_block: the ADDLN block's out_proj writes the hidden rows, not the residual buffers");
     if (sl == 8)
-      ZMI_CHECK((launch_block<8, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s,
-                                                                     oproj)));
+      ZMI_CHECK(addln ? (launch_block<8, zmi_gemv::PRO_ADDLN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units,
+                                                                                 (uint64_t*)gran, pf, s, oproj))
+                      : (launch_block<8, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran,
+                                                                              pf, s, oproj)));
     else
-      ZMI_CHECK((launch_block<24, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf,
-                                                                      s, oproj)));
+      ZMI_CHECK(addln ? (launch_block<24, zmi_gemv::PRO_ADDLN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units,
+                                                                                  (uint64_t*)gran, pf, s, oproj))
+                      : (launch_block<24, zmi_gemv::PRO_LN, FORM_SPLIT, true>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran,
+                                                                               pf, s, oproj)));
     return 0;
   }
 #define ZMI_BLK(S_, P_, F_) launch_block<S_, P_, F_>(a, n_cb, n_qkv, at, n_units, (uint64_t*)gran, pf, s)

@@ -247,8 +247,9 @@ __device__ __forceinline__ void gemv_body(const ZmiGemvArgs& a, int n_cb, int n_
   static_assert(RT == 8 || RT == 16, "row tile");
   static_assert(!FUSE || EPI == ZMI_EPI_QKV || EPI == ZMI_EPI_STORE || FUSE == 3, "in-launch hand-off: QKV or plain store");
   static_assert(FUSE != 2 || NTW, "the store hand-off runs on single-tile (decode) launches");
-  static_assert(FUSE != 3 || (NTW && EPI == ZMI_EPI_RESIDUAL && PRO == PRO_PLAIN && K == 2048 && RT == 16),
-                "the gathered-input form is zmi_attn_block's out_proj role (one tile, plain, residual epilogue)");
+  static_assert(FUSE != 3 || (NTW && (EPI == ZMI_EPI_RESIDUAL || EPI == ZMI_EPI_STORE) && PRO == PRO_PLAIN && K == 2048 &&
+                              RT == 16),
+                "the gathered-input form is zmi_attn_block's out_proj role (one tile, plain, residual or store epilogue)");
 
   // block -> (column block, group of rpw row tiles): the groups of one column block take ids 8 apart.
   // A workgroup keeps its weight slice in registers and runs its row tiles one after the other, each

@@ -95,6 +95,8 @@ class HybridEngine(HipEngine):
         # rows per workgroup at 2 rows) instead of y and the gate (GRMS: 48 KB); the same bits
         self.grms_g = True
         self.prefetch_blocks, self.prefetch_fc1_mb = 192, 0  # the MHA blocks' out_proj prefetch (measured in round 2)
+        # the MHA blocks' out_proj inside the fused block (round 6; the prefetch above then stays off)
+        self.attn_oproj_mha = True
 
     def _kv_layers(self) -> int:
         return len(self.attn_idx)
@@ -304,16 +306,22 @@ class HybridEngine(HipEngine):
                     qkv = normed_gemv(self._gemv(lw["qkv"], x_in, rows, qkv_n, d, _lib.EPI_QKV, self.q, qd,
                                                  kv=(self.kc[j], self.vc[j]), row_kv=self.row_kv,
                                                  row_pos=self.row_pos), ln1, i == 0)
+                    # out_proj as the fused block's fourth role (zmi_attn_block_oproj, plain store into the hidden rows)
+                    oproj = (self._use_attn_block(rows, form) and self.attn_oproj_mha and form in ("split", "split24")
+                             and qd == d)
                     if self._use_attn_block(rows, form):
                         pf = _lib.Prefetch()
-                        if self.prefetch_blocks > 0:  # out_proj's weights into the Infinity Cache meanwhile
+                        if self.prefetch_blocks > 0 and not oproj:  # out_proj's weights into the Infinity Cache meanwhile
                             pf.ptr[0], pf.bytes[0] = lw["out"].data_ptr(), lw["out"].numel() * 2
                             pf.sink, pf.blocks = self.blk_err[2:].data_ptr(), self.prefetch_blocks
-                        plan.append(("attnblk", (qkv[1][0], j, pf, self._block_slices(form))))
+                        o_item = self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)
+                        plan.append(("attnblk", (qkv[1][0], j, pf, self._block_slices(form)) +
+                                     ((o_item[0],) if oproj else ())))
                     else:
                         plan.append(qkv)
                         plan.append(("attn", j))
-                    plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)))
+                    if not oproj:
+                        plan.append(("gemv", self._gemv(lw["out"], self.attn, rows, d, qd, _lib.EPI_STORE, self.hid, d)))
                 else:
                     inp = normed_gemv(self._gemv(lw["in_proj"], x_in, rows, md["d_in_proj"], d, _lib.EPI_STORE,
                                                  self.zx, md["d_in_proj"]), ln1, i == 0)
