@@ -795,6 +795,9 @@ struct XcImg {
   static constexpr size_t BYTES = (QKV + (size_t)QKV_GRAN * 4 + 15) / 16 * 16;
 };
 
+#ifndef ZMI_XC_QKV_SLEEP
+#define ZMI_XC_QKV_SLEEP 8  // the chunk-split form's q / K / V poll: s_sleep between its two sweeps in flight
+#endif
 template <int XCH, bool OPROJ>
 __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
   using X = XcG<XCH>;
@@ -862,7 +865,7 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
         for (int i = 0; i < 6; ++i) qkv_lds[lane + 64 * i] = (uint32_t)g[i];
       };
       sweep(A);
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(ZMI_XC_QKV_SLEEP);
       sweep(B);
       for (unsigned spins = 0;; spins += 2) {
         if (ready(A)) {
@@ -870,13 +873,13 @@ __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, c
           break;
         }
         sweep(A);
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(ZMI_XC_QKV_SLEEP);
         if (ready(B)) {
           stage(B);
           break;
         }
         sweep(B);
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(ZMI_XC_QKV_SLEEP);
         if (spins > XS_SPIN) {
           give_up(a);
           stage(A);
