@@ -796,7 +796,8 @@ struct XcImg {
 };
 
 #ifndef ZMI_XC_QKV_SLEEP
-#define ZMI_XC_QKV_SLEEP 8  // the chunk-split form's q / K / V poll: s_sleep between its two sweeps in flight
+#define ZMI_XC_QKV_SLEEP 2  // the chunk-split form's q / K / V poll: s_sleep between its two sweeps in flight (8 before
+                            // round 6's end: C2 step 890-902 vs 881-884 us with 2, 889-898 with 4, 905-919 with 16)
 #endif
 template <int XCH, bool OPROJ>
 __device__ __forceinline__ void xc_body(const AttnArgs& a, int n_units, int b, char* smem, uint64_t* gran) {
